@@ -1,0 +1,558 @@
+// hspmv_api.cpp -- device runtime behind the C ABI (include/hspmv.h):
+// handles, uploads, launch planning, the reference timing protocol and the
+// multi-GPU row-range partition with RCCL over xGMI.
+//
+// Replaces the CSRk_Graph device plumbing of the reference
+// (cuda-spmv-csrk/hip/csrk.cu:92-113, 531-641, 722-870): device buffers are
+// owned by a handle instead of process globals, every HIP/RCCL status is
+// checked, and there is one stream per GPU instead of the default stream +
+// hipDeviceSynchronize.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <memory>
+#include <vector>
+
+#include "hspmv_common.h"
+#include "hspmv_internal.h"
+
+namespace hspmv {
+namespace {
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess)                                                          \
+      return set_error(HSPMV_E_HIP, "%s failed: %s (%s:%d)", #expr,                \
+                       hipGetErrorString(_e), __FILE__, __LINE__);                 \
+  } while (0)
+
+#define RCCL_TRY(expr)                                                             \
+  do {                                                                             \
+    ncclResult_t _r = (expr);                                                      \
+    if (_r != ncclSuccess)                                                         \
+      return set_error(HSPMV_E_RCCL, "%s failed: %s", #expr, ncclGetErrorString(_r)); \
+  } while (0)
+
+// One row-range shard on one GPU.
+struct Shard {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int64_t row0 = 0;  // first global row
+  DevCSR A;          // device view (rows rebased to 0)
+  LaunchPlan plan;
+  double mean_rows_per_ssr = 0.0;
+  // owned device memory
+  int32_t *d_rp = nullptr, *d_ci = nullptr, *d_outer = nullptr, *d_inner = nullptr;
+  void *d_val = nullptr;
+  void *d_x = nullptr;     // own x (n entries)
+  void *d_y = nullptr;     // own y (m_shard entries) -- or a slice of d_yfull
+  void *d_yfull = nullptr; // multi-GPU: padded all-gather buffer P*max_rows
+  const void *x = nullptr; // x in use (own or bound)
+  void *y = nullptr;       // y in use (own or bound)
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int64_t bytes = 0;
+};
+
+}  // namespace
+}  // namespace hspmv
+
+struct hspmv_handle {
+  std::vector<hspmv::Shard> shards;
+  int64_t m = 0, n = 0, nnz = 0;
+  int dtype = HSPMV_F64;
+  int64_t n_ssr = 0, n_sr = 0;
+  unsigned flags = 0;
+  bool x_set = false;
+  bool borrowed = false;  // HSPMV_FLAG_DEVICE_PTRS: matrix arrays not owned
+  int64_t max_rows = 0;   // multi-GPU padding for the y all-gather
+  std::vector<ncclComm_t> comms;
+};
+
+using namespace hspmv;
+
+namespace {
+
+template <typename T>
+int dev_alloc(T **p, size_t bytes, int64_t *acc) {
+  *p = nullptr;
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc((void **)p, bytes);
+  if (e != hipSuccess)
+    return set_error(HSPMV_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  *acc += (int64_t)bytes;
+  return HSPMV_OK;
+}
+
+void free_shard(Shard &s, bool borrowed) {
+  (void)hipSetDevice(s.device);
+  if (!borrowed) {
+    (void)hipFree(s.d_rp);
+    (void)hipFree(s.d_ci);
+    (void)hipFree(s.d_val);
+    (void)hipFree(s.d_outer);
+    (void)hipFree(s.d_inner);
+  }
+  (void)hipFree(s.d_x);
+  if (!s.d_yfull) (void)hipFree(s.d_y);
+  (void)hipFree(s.d_yfull);
+  if (s.ev0) (void)hipEventDestroy(s.ev0);
+  if (s.ev1) (void)hipEventDestroy(s.ev1);
+  if (s.own_stream && s.stream) (void)hipStreamDestroy(s.stream);
+  s = Shard();
+}
+
+// Uploads rows [r0, r1) of A (and the matching slice of the maps) to shard s.
+int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_t r0, int64_t r1,
+                 int64_t ssr0, int64_t ssr1, int64_t y_rows_alloc) {
+  const size_t sv = dtype_size(A->dtype);
+  const int64_t m = r1 - r0;
+  const int64_t k0 = A->row_ptr[r0], k1 = A->row_ptr[r1];
+  const int64_t nnz = k1 - k0;
+  HIP_TRY(hipSetDevice(s.device));
+  s.row0 = r0;
+  int rc;
+  if ((rc = dev_alloc(&s.d_rp, 4 * (size_t)(m + 1), &s.bytes))) return rc;
+  if ((rc = dev_alloc(&s.d_ci, 4 * (size_t)nnz, &s.bytes))) return rc;
+  if ((rc = dev_alloc(&s.d_val, sv * (size_t)nnz, &s.bytes))) return rc;
+  if ((rc = dev_alloc(&s.d_x, sv * (size_t)A->n, &s.bytes))) return rc;
+  if (y_rows_alloc > 0) {
+    if ((rc = dev_alloc(&s.d_y, sv * (size_t)y_rows_alloc, &s.bytes))) return rc;
+  }
+  std::vector<int32_t> rp((size_t)(m + 1));
+  for (int64_t i = 0; i <= m; ++i) rp[i] = (int32_t)(A->row_ptr[r0 + i] - k0);
+  HIP_TRY(hipMemcpy(s.d_rp, rp.data(), 4 * (size_t)(m + 1), hipMemcpyHostToDevice));
+  if (nnz) {
+    HIP_TRY(hipMemcpy(s.d_ci, A->col_idx + k0, 4 * (size_t)nnz, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s.d_val, (const char *)A->val + sv * k0, sv * (size_t)nnz,
+                      hipMemcpyHostToDevice));
+  }
+  s.A.m = (int32_t)m;
+  s.A.n = A->n;
+  s.A.nnz = nnz;
+  s.A.row_ptr = s.d_rp;
+  s.A.col_idx = s.d_ci;
+  s.A.val = s.d_val;
+  if (mp && mp->n_ssr > 0) {
+    const int64_t nssr = ssr1 - ssr0;
+    const int64_t sr0 = mp->outer[ssr0], sr1 = mp->outer[ssr1];
+    const int64_t nsr = sr1 - sr0;
+    std::vector<int32_t> o((size_t)(nssr + 1)), in((size_t)(nsr + 1));
+    for (int64_t i = 0; i <= nssr; ++i) o[i] = (int32_t)(mp->outer[ssr0 + i] - sr0);
+    for (int64_t i = 0; i <= nsr; ++i) in[i] = (int32_t)(mp->inner[sr0 + i] - r0);
+    if ((rc = dev_alloc(&s.d_outer, 4 * (size_t)(nssr + 1), &s.bytes))) return rc;
+    if ((rc = dev_alloc(&s.d_inner, 4 * (size_t)(nsr + 1), &s.bytes))) return rc;
+    HIP_TRY(hipMemcpy(s.d_outer, o.data(), 4 * (size_t)(nssr + 1), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s.d_inner, in.data(), 4 * (size_t)(nsr + 1), hipMemcpyHostToDevice));
+    s.A.n_ssr = (int32_t)nssr;
+    s.A.n_sr = (int32_t)nsr;
+    s.A.outer = s.d_outer;
+    s.A.inner = s.d_inner;
+    s.mean_rows_per_ssr = nssr ? (double)m / (double)nssr : 0.0;
+  }
+  return HSPMV_OK;
+}
+
+int finish_shard(Shard &s, int dtype, unsigned flags, void *stream) {
+  HIP_TRY(hipSetDevice(s.device));
+  if (stream) {
+    s.stream = (hipStream_t)stream;
+    s.own_stream = false;
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    s.own_stream = true;
+  }
+  HIP_TRY(hipEventCreate(&s.ev0));
+  HIP_TRY(hipEventCreate(&s.ev1));
+  s.plan = plan_launch(s.A, dtype, flags, s.mean_rows_per_ssr);
+  s.x = s.d_x;
+  s.y = s.d_y;
+  return HSPMV_OK;
+}
+
+int check_handle(hspmv_handle *h) {
+  if (!h || h->shards.empty()) return set_error(HSPMV_E_INVALID, "invalid handle");
+  return HSPMV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hspmv_device_count(int *count) {
+  clear_error();
+  if (!count) return set_error(HSPMV_E_INVALID, "NULL argument");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *count = 0;
+    return set_error(HSPMV_E_NODEV, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *count = c;
+  return HSPMV_OK;
+}
+
+int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps,
+                           int device, void *stream, unsigned flags) {
+  clear_error();
+  if (!hp) return set_error(HSPMV_E_INVALID, "NULL handle pointer");
+  *hp = nullptr;
+  const bool devptrs = (flags & HSPMV_FLAG_DEVICE_PTRS) != 0;
+  if (!A) return set_error(HSPMV_E_INVALID, "matrix is NULL");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+    return set_error(HSPMV_E_NODEV, "no HIP device available");
+  if (device < 0 || device >= ndev)
+    return set_error(HSPMV_E_NODEV, "device %d out of range (have %d)", device, ndev);
+  std::unique_ptr<hspmv_handle> h(new hspmv_handle());
+  h->m = A->m; h->n = A->n; h->nnz = A->nnz; h->dtype = A->dtype; h->flags = flags;
+  h->shards.resize(1);
+  Shard &s = h->shards[0];
+  s.device = device;
+  int rc;
+  if (!devptrs) {
+    if ((rc = validate_host_csr(A, true))) return rc;
+    if ((rc = validate_host_maps(maps, A->m))) return rc;
+    if (maps && maps->n_ssr > 0) { h->n_ssr = maps->n_ssr; h->n_sr = maps->n_sr; }
+    if ((rc = upload_shard(s, A, maps, 0, A->m, 0, maps ? maps->n_ssr : 0, A->m))) {
+      free_shard(s, false);
+      return rc;
+    }
+  } else {
+    // Borrowed device arrays: validate what the kernels index with (row_ptr
+    // and the maps) on the host before the first launch.
+    h->borrowed = true;
+    if (A->m < 0 || A->n < 0 || A->nnz < 0 || A->m >= INT32_MAX || A->nnz >= INT32_MAX ||
+        (A->dtype != HSPMV_F32 && A->dtype != HSPMV_F64) || !A->row_ptr)
+      return set_error(HSPMV_E_INVALID, "bad device matrix description");
+    HIP_TRY(hipSetDevice(device));
+    std::vector<int32_t> rp((size_t)(A->m + 1));
+    HIP_TRY(hipMemcpy(rp.data(), A->row_ptr, 4 * (size_t)(A->m + 1), hipMemcpyDeviceToHost));
+    hspmv_csr view = *A;
+    view.row_ptr = rp.data();
+    view.col_idx = nullptr;
+    view.val = nullptr;
+    if (A->nnz > 0 && (!A->col_idx || !A->val)) return set_error(HSPMV_E_INVALID, "col/val NULL");
+    if ((rc = validate_host_csr(&view, false)) != HSPMV_OK && A->nnz > 0) return rc;
+    s.A.m = (int32_t)A->m; s.A.n = A->n; s.A.nnz = A->nnz;
+    s.A.row_ptr = A->row_ptr; s.A.col_idx = A->col_idx; s.A.val = A->val;
+    if (maps && maps->n_ssr > 0) {
+      std::vector<int32_t> o((size_t)(maps->n_ssr + 1)), in((size_t)(maps->n_sr + 1));
+      HIP_TRY(hipMemcpy(o.data(), maps->outer, 4 * o.size(), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(in.data(), maps->inner, 4 * in.size(), hipMemcpyDeviceToHost));
+      hspmv_csr3_maps mv = {maps->n_ssr, maps->n_sr, o.data(), in.data()};
+      if ((rc = validate_host_maps(&mv, A->m))) return rc;
+      s.A.n_ssr = (int32_t)maps->n_ssr; s.A.n_sr = (int32_t)maps->n_sr;
+      s.A.outer = maps->outer; s.A.inner = maps->inner;
+      s.mean_rows_per_ssr = (double)A->m / (double)maps->n_ssr;
+      h->n_ssr = maps->n_ssr; h->n_sr = maps->n_sr;
+    }
+    const size_t sv = dtype_size(A->dtype);
+    if ((rc = dev_alloc(&s.d_x, sv * (size_t)A->n, &s.bytes))) return rc;
+    if ((rc = dev_alloc(&s.d_y, sv * (size_t)A->m, &s.bytes))) return rc;
+  }
+  if ((rc = finish_shard(s, A->dtype, flags, stream))) {
+    free_shard(s, h->borrowed);
+    return rc;
+  }
+  *hp = h.release();
+  return HSPMV_OK;
+}
+
+int hspmv_create(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps, int num_gpus,
+                 unsigned flags) {
+  clear_error();
+  if (!hp) return set_error(HSPMV_E_INVALID, "NULL handle pointer");
+  *hp = nullptr;
+  if (flags & HSPMV_FLAG_DEVICE_PTRS)
+    return set_error(HSPMV_E_INVALID, "device pointers need hspmv_create_on_device");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+    return set_error(HSPMV_E_NODEV, "no HIP device available");
+  if (num_gpus <= 0) num_gpus = ndev;
+  if (num_gpus > ndev)
+    return set_error(HSPMV_E_NODEV, "%d GPUs requested, %d visible", num_gpus, ndev);
+  if (num_gpus == 1) return hspmv_create_on_device(hp, A, maps, 0, nullptr, flags);
+  int rc;
+  if ((rc = validate_host_csr(A, true))) return rc;
+  if ((rc = validate_host_maps(maps, A->m))) return rc;
+  const bool csr3 = maps && maps->n_ssr > 0;
+  std::unique_ptr<hspmv_handle> h(new hspmv_handle());
+  h->m = A->m; h->n = A->n; h->nnz = A->nnz; h->dtype = A->dtype; h->flags = flags;
+  if (csr3) { h->n_ssr = maps->n_ssr; h->n_sr = maps->n_sr; }
+  std::vector<int64_t> splits((size_t)num_gpus + 1);
+  if ((rc = hspmv_partition_rows(A->m, A->row_ptr, csr3 ? maps : nullptr, num_gpus, splits.data())))
+    return rc;
+  // super-super-row index of each split (CSR-3 partitions on SSR boundaries)
+  std::vector<int64_t> ssr_split((size_t)num_gpus + 1, 0);
+  if (csr3) {
+    int64_t s = 0;
+    for (int p = 0; p <= num_gpus; ++p) {
+      while (s < maps->n_ssr && maps->inner[maps->outer[s]] < splits[p]) ++s;
+      ssr_split[p] = s;
+    }
+    ssr_split[num_gpus] = maps->n_ssr;
+  }
+  int64_t max_rows = 0;
+  for (int p = 0; p < num_gpus; ++p) max_rows = std::max(max_rows, splits[p + 1] - splits[p]);
+  h->max_rows = max_rows;
+  h->shards.resize((size_t)num_gpus);
+  const size_t sv = dtype_size(A->dtype);
+  auto cleanup = [&]() {
+    for (auto &s : h->shards) free_shard(s, false);
+  };
+  for (int p = 0; p < num_gpus; ++p) {
+    Shard &s = h->shards[p];
+    s.device = p;
+    if ((rc = upload_shard(s, A, maps, splits[p], splits[p + 1], ssr_split[p], ssr_split[p + 1], 0))) {
+      cleanup();
+      return rc;
+    }
+    // y lives in this GPU's slot of a padded [P][max_rows] all-gather buffer
+    if ((rc = dev_alloc(&s.d_yfull, sv * (size_t)(max_rows * num_gpus), &s.bytes))) {
+      cleanup();
+      return rc;
+    }
+    s.d_y = (char *)s.d_yfull + sv * (size_t)(max_rows * p);
+    if ((rc = finish_shard(s, A->dtype, flags, nullptr))) {
+      cleanup();
+      return rc;
+    }
+  }
+  h->comms.resize((size_t)num_gpus);
+  std::vector<int> devs((size_t)num_gpus);
+  for (int p = 0; p < num_gpus; ++p) devs[p] = p;
+  ncclResult_t r = ncclCommInitAll(h->comms.data(), num_gpus, devs.data());
+  if (r != ncclSuccess) {
+    cleanup();
+    h->comms.clear();
+    return set_error(HSPMV_E_RCCL, "ncclCommInitAll: %s", ncclGetErrorString(r));
+  }
+  *hp = h.release();
+  return HSPMV_OK;
+}
+
+static int bcast_x(hspmv_handle *h) {
+  if (h->shards.size() < 2) return HSPMV_OK;
+  const ncclDataType_t dt = h->dtype == HSPMV_F64 ? ncclFloat64 : ncclFloat32;
+  RCCL_TRY(ncclGroupStart());
+  for (size_t p = 0; p < h->shards.size(); ++p) {
+    Shard &s = h->shards[p];
+    RCCL_TRY(ncclBroadcast(h->shards[0].d_x, s.d_x, (size_t)h->n, dt, 0, h->comms[p], s.stream));
+  }
+  RCCL_TRY(ncclGroupEnd());
+  return HSPMV_OK;
+}
+
+static int gather_y(hspmv_handle *h) {
+  if (h->shards.size() < 2) return HSPMV_OK;
+  const ncclDataType_t dt = h->dtype == HSPMV_F64 ? ncclFloat64 : ncclFloat32;
+  RCCL_TRY(ncclGroupStart());
+  for (size_t p = 0; p < h->shards.size(); ++p) {
+    Shard &s = h->shards[p];
+    RCCL_TRY(ncclAllGather(s.d_y, s.d_yfull, (size_t)h->max_rows, dt, h->comms[p], s.stream));
+  }
+  RCCL_TRY(ncclGroupEnd());
+  return HSPMV_OK;
+}
+
+int hspmv_set_x(hspmv_handle *h, const void *x_host) {
+  clear_error();
+  int rc;
+  if ((rc = check_handle(h))) return rc;
+  if (!x_host && h->n > 0) return set_error(HSPMV_E_INVALID, "x is NULL");
+  const size_t bytes = dtype_size(h->dtype) * (size_t)h->n;
+  Shard &s0 = h->shards[0];
+  HIP_TRY(hipSetDevice(s0.device));
+  if (bytes) {
+    HIP_TRY(hipMemcpyAsync(s0.d_x, x_host, bytes, hipMemcpyHostToDevice, s0.stream));
+    HIP_TRY(hipStreamSynchronize(s0.stream));
+  }
+  if ((rc = bcast_x(h))) return rc;
+  for (auto &s : h->shards) {
+    HIP_TRY(hipSetDevice(s.device));
+    HIP_TRY(hipStreamSynchronize(s.stream));
+    s.x = s.d_x;
+  }
+  h->x_set = true;
+  return HSPMV_OK;
+}
+
+int hspmv_bind_x_device(hspmv_handle *h, const void *x_dev) {
+  clear_error();
+  int rc;
+  if ((rc = check_handle(h))) return rc;
+  if (h->shards.size() != 1) return set_error(HSPMV_E_STATE, "bind needs a single-device handle");
+  h->shards[0].x = x_dev ? x_dev : h->shards[0].d_x;
+  h->x_set = x_dev != nullptr || h->x_set;
+  return HSPMV_OK;
+}
+
+int hspmv_bind_y_device(hspmv_handle *h, void *y_dev) {
+  clear_error();
+  int rc;
+  if ((rc = check_handle(h))) return rc;
+  if (h->shards.size() != 1) return set_error(HSPMV_E_STATE, "bind needs a single-device handle");
+  h->shards[0].y = y_dev ? y_dev : h->shards[0].d_y;
+  return HSPMV_OK;
+}
+
+void *hspmv_x_device(hspmv_handle *h, int gpu) {
+  if (!h || gpu < 0 || gpu >= (int)h->shards.size()) return nullptr;
+  return (void *)h->shards[gpu].x;
+}
+
+void *hspmv_y_device(hspmv_handle *h, int gpu) {
+  if (!h || gpu < 0 || gpu >= (int)h->shards.size()) return nullptr;
+  return h->shards[gpu].y;
+}
+
+int hspmv_spmv(hspmv_handle *h) {
+  int rc;
+  if ((rc = check_handle(h))) return rc;
+  if (!h->x_set) return set_error(HSPMV_E_STATE, "x not set (hspmv_set_x / hspmv_bind_x_device)");
+  for (auto &s : h->shards) {
+    HIP_TRY(hipSetDevice(s.device));
+    hipError_t e = launch_spmv(s.A, h->dtype, s.plan, s.x, s.y, s.stream);
+    if (e != hipSuccess)
+      return set_error(HSPMV_E_HIP, "SpMV launch on GPU %d failed: %s", s.device, hipGetErrorString(e));
+  }
+  return HSPMV_OK;
+}
+
+int hspmv_synchronize(hspmv_handle *h) {
+  clear_error();
+  int rc;
+  if ((rc = check_handle(h))) return rc;
+  for (auto &s : h->shards) {
+    HIP_TRY(hipSetDevice(s.device));
+    HIP_TRY(hipStreamSynchronize(s.stream));
+  }
+  return HSPMV_OK;
+}
+
+int hspmv_run(hspmv_handle *h, int warmup, int iters, hspmv_timing *out) {
+  clear_error();
+  int rc;
+  if ((rc = check_handle(h))) return rc;
+  if (!out || iters < 1 || warmup < 0) return set_error(HSPMV_E_INVALID, "bad arguments");
+  for (int i = 0; i < warmup; ++i) {
+    if ((rc = hspmv_spmv(h))) return rc;
+    if ((rc = hspmv_synchronize(h))) return rc;
+  }
+  double tmin = 1e30, tmax = 0, tsum = 0, wmin = 1e30, wmax = 0, wsum = 0;
+  for (int i = 0; i < iters; ++i) {
+    auto tic = std::chrono::steady_clock::now();
+    for (auto &s : h->shards) {
+      HIP_TRY(hipSetDevice(s.device));
+      HIP_TRY(hipEventRecord(s.ev0, s.stream));
+      hipError_t e = launch_spmv(s.A, h->dtype, s.plan, s.x, s.y, s.stream);
+      if (e != hipSuccess)
+        return set_error(HSPMV_E_HIP, "SpMV launch failed: %s", hipGetErrorString(e));
+      HIP_TRY(hipEventRecord(s.ev1, s.stream));
+    }
+    double dev = 0.0;
+    for (auto &s : h->shards) {
+      HIP_TRY(hipSetDevice(s.device));
+      HIP_TRY(hipEventSynchronize(s.ev1));
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, s.ev0, s.ev1));
+      dev = std::max(dev, (double)ms * 1e-3);
+    }
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - tic).count();
+    tmin = std::min(tmin, dev); tmax = std::max(tmax, dev); tsum += dev;
+    wmin = std::min(wmin, wall); wmax = std::max(wmax, wall); wsum += wall;
+  }
+  memset(out, 0, sizeof(*out));
+  out->t_min = tmin; out->t_max = tmax; out->t_avg = tsum / iters;
+  out->wall_min = wmin; out->wall_max = wmax; out->wall_avg = wsum / iters;
+  out->gflops = tmin > 0 ? 2.0 * (double)h->nnz / tmin * 1e-9 : 0.0;
+  out->gbps_alg = tmin > 0 ? hspmv_alg_bytes(h->m, h->n, h->nnz, h->dtype, h->n_ssr, h->n_sr) / tmin * 1e-9 : 0.0;
+  out->iters = iters;
+  out->num_gpus = (int32_t)h->shards.size();
+  return HSPMV_OK;
+}
+
+int hspmv_get_y(hspmv_handle *h, void *y_host) {
+  clear_error();
+  int rc;
+  if ((rc = check_handle(h))) return rc;
+  if (!y_host && h->m > 0) return set_error(HSPMV_E_INVALID, "y is NULL");
+  const size_t sv = dtype_size(h->dtype);
+  if (h->shards.size() == 1) {
+    Shard &s = h->shards[0];
+    HIP_TRY(hipSetDevice(s.device));
+    if (h->m) HIP_TRY(hipMemcpyAsync(y_host, s.y, sv * (size_t)h->m, hipMemcpyDeviceToHost, s.stream));
+    HIP_TRY(hipStreamSynchronize(s.stream));
+    return HSPMV_OK;
+  }
+  // RCCL all-gather of the padded shards, then unpad GPU 0's copy.
+  if ((rc = gather_y(h))) return rc;
+  if ((rc = hspmv_synchronize(h))) return rc;
+  Shard &s0 = h->shards[0];
+  HIP_TRY(hipSetDevice(s0.device));
+  std::vector<char> full(sv * (size_t)(h->max_rows * (int64_t)h->shards.size()));
+  HIP_TRY(hipMemcpy(full.data(), s0.d_yfull, full.size(), hipMemcpyDeviceToHost));
+  for (size_t p = 0; p < h->shards.size(); ++p) {
+    const Shard &s = h->shards[p];
+    memcpy((char *)y_host + sv * (size_t)s.row0, full.data() + sv * (size_t)(h->max_rows * (int64_t)p),
+           sv * (size_t)s.A.m);
+  }
+  return HSPMV_OK;
+}
+
+int hspmv_exchange(hspmv_handle *h, double *bcast_s, double *gather_s) {
+  clear_error();
+  int rc;
+  if ((rc = check_handle(h))) return rc;
+  if (bcast_s) {
+    if ((rc = hspmv_synchronize(h))) return rc;
+    auto tic = std::chrono::steady_clock::now();
+    if ((rc = bcast_x(h))) return rc;
+    if ((rc = hspmv_synchronize(h))) return rc;
+    *bcast_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tic).count();
+  }
+  if (gather_s) {
+    if ((rc = hspmv_synchronize(h))) return rc;
+    auto tic = std::chrono::steady_clock::now();
+    if ((rc = gather_y(h))) return rc;
+    if ((rc = hspmv_synchronize(h))) return rc;
+    *gather_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tic).count();
+  }
+  return HSPMV_OK;
+}
+
+int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
+  clear_error();
+  int rc;
+  if ((rc = check_handle(h))) return rc;
+  if (!out) return set_error(HSPMV_E_INVALID, "NULL output");
+  memset(out, 0, sizeof(*out));
+  const Shard &s = h->shards[0];
+  out->kernel = s.plan.kernel;
+  out->lanes = s.plan.lanes;
+  out->waves_per_block = s.plan.waves_per_block;
+  out->num_gpus = (int32_t)h->shards.size();
+  out->blocks = s.plan.blocks;
+  out->alg_bytes = hspmv_alg_bytes(h->m, h->n, h->nnz, h->dtype, h->n_ssr, h->n_sr);
+  out->flops = 2.0 * (double)h->nnz;
+  for (auto &sh : h->shards) out->device_bytes += sh.bytes;
+  return HSPMV_OK;
+}
+
+void hspmv_destroy(hspmv_handle *h) {
+  if (!h) return;
+  for (auto &s : h->shards) {
+    (void)hipSetDevice(s.device);
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+  }
+  for (auto c : h->comms) (void)ncclCommDestroy(c);
+  for (auto &s : h->shards) free_shard(s, h->borrowed);
+  delete h;
+}
+
+}  // extern "C"

@@ -1,0 +1,680 @@
+// hspmv_io.cpp -- host side of libhspmv that needs no GPU: error state,
+// validation, the .csr / .csr3 text readers and writers, the binary cache,
+// the CSR-3 map builder, launch-parameter heuristics and the row partitioner.
+//
+// The readers replace my_read_csr (spmv-csr/spmv.c:11-57) and my_read_csr3
+// (reformat-csr-to-csr3/stats.c:10-79), whose per-token fscanf takes minutes
+// at 200 M nonzeros (SURVEY.md §7 hard part (f)).  Here the file is read in
+// one pass, split into chunks on whitespace, tokens are counted per chunk in
+// parallel, prefix-summed, and parsed in parallel with std::from_chars
+// (correctly rounded, i.e. the same float as the reference's fscanf("%f")).
+#include <errno.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <charconv>
+#include <cmath>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "hspmv_common.h"
+
+namespace hspmv {
+
+static thread_local std::string g_err;
+
+int set_error(int code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+void clear_error() { g_err.clear(); }
+
+int validate_host_csr(const hspmv_csr *A, bool check_cols) {
+  if (!A) return set_error(HSPMV_E_INVALID, "matrix is NULL");
+  if (A->m < 0 || A->n < 0 || A->nnz < 0)
+    return set_error(HSPMV_E_INVALID, "negative dimension (m=%lld n=%lld nnz=%lld)",
+                     (long long)A->m, (long long)A->n, (long long)A->nnz);
+  if (A->m >= INT32_MAX || A->n >= INT32_MAX || A->nnz >= INT32_MAX)
+    return set_error(HSPMV_E_INVALID, "dimensions exceed int32 indexing");
+  if (A->dtype != HSPMV_F32 && A->dtype != HSPMV_F64)
+    return set_error(HSPMV_E_INVALID, "unknown dtype %d", A->dtype);
+  if (!A->row_ptr) return set_error(HSPMV_E_INVALID, "row_ptr is NULL");
+  if (A->nnz > 0 && (!A->col_idx || !A->val))
+    return set_error(HSPMV_E_INVALID, "col_idx/val is NULL");
+  if (A->row_ptr[0] != 0)
+    return set_error(HSPMV_E_INVALID, "row_ptr[0] = %d (expected 0)", A->row_ptr[0]);
+  for (int64_t i = 0; i < A->m; ++i)
+    if (A->row_ptr[i + 1] < A->row_ptr[i])
+      return set_error(HSPMV_E_INVALID, "row_ptr decreases at row %lld", (long long)i);
+  if (A->row_ptr[A->m] != A->nnz)
+    return set_error(HSPMV_E_INVALID, "row_ptr[m] = %d but nnz = %lld",
+                     A->row_ptr[A->m], (long long)A->nnz);
+  if (check_cols) {
+    for (int64_t k = 0; k < A->nnz; ++k) {
+      const int32_t c = A->col_idx[k];
+      if (c < 0 || c >= A->n)
+        return set_error(HSPMV_E_INVALID, "col_idx[%lld] = %d out of [0, %lld)",
+                         (long long)k, c, (long long)A->n);
+    }
+  }
+  return HSPMV_OK;
+}
+
+int validate_host_maps(const hspmv_csr3_maps *mp, int64_t m) {
+  if (!mp) return HSPMV_OK;
+  if (mp->n_ssr < 0 || mp->n_sr < 0 || !mp->outer || !mp->inner)
+    return set_error(HSPMV_E_INVALID, "CSR-3 maps incomplete");
+  if (mp->outer[0] != 0 || mp->outer[mp->n_ssr] != mp->n_sr)
+    return set_error(HSPMV_E_INVALID, "outer map must run 0..n_sr (got %d..%d, n_sr=%lld)",
+                     mp->outer[0], mp->outer[mp->n_ssr], (long long)mp->n_sr);
+  if (mp->inner[0] != 0 || mp->inner[mp->n_sr] != m)
+    return set_error(HSPMV_E_INVALID, "inner map must run 0..m (got %d..%d, m=%lld)",
+                     mp->inner[0], mp->inner[mp->n_sr], (long long)m);
+  for (int64_t s = 0; s < mp->n_ssr; ++s)
+    if (mp->outer[s + 1] < mp->outer[s])
+      return set_error(HSPMV_E_INVALID, "outer map decreases at %lld", (long long)s);
+  for (int64_t s = 0; s < mp->n_sr; ++s)
+    if (mp->inner[s + 1] < mp->inner[s])
+      return set_error(HSPMV_E_INVALID, "inner map decreases at %lld", (long long)s);
+  return HSPMV_OK;
+}
+
+// ------------------------------------------------------------ text parsing
+
+namespace {
+
+inline bool is_space(char c) { return c == ' ' || c == '\n' || c == '\t' || c == '\r' || c == '\f' || c == '\v'; }
+
+struct FileBuf {
+  std::vector<char> data;
+  bool ok = false;
+};
+
+FileBuf slurp(const char *path) {
+  FileBuf fb;
+  FILE *fp = fopen(path, "rb");
+  if (!fp) return fb;
+  fseek(fp, 0, SEEK_END);
+  long sz = ftell(fp);
+  fseek(fp, 0, SEEK_SET);
+  if (sz < 0) { fclose(fp); return fb; }
+  fb.data.resize((size_t)sz + 1);
+  size_t got = fread(fb.data.data(), 1, (size_t)sz, fp);
+  fclose(fp);
+  fb.data[got] = 0;
+  fb.data.resize(got + 1);
+  fb.ok = true;
+  return fb;
+}
+
+int num_threads() {
+  unsigned hc = std::thread::hardware_concurrency();
+  const char *env = getenv("HSPMV_IO_THREADS");
+  int t = env ? atoi(env) : (int)(hc ? hc : 4);
+  if (t > 16) t = 16;  // GPU-box CPU share (16); enough to saturate parsing
+  return t < 1 ? 1 : t;
+}
+
+// Parses header integers sequentially; returns pointer just after them.
+const char *parse_header(const char *p, const char *end, long long *vals, int count) {
+  for (int i = 0; i < count; ++i) {
+    while (p < end && is_space(*p)) ++p;
+    auto r = std::from_chars(p, end, vals[i]);
+    if (r.ec != std::errc()) return nullptr;
+    p = r.ptr;
+  }
+  return p;
+}
+
+// Section table: tokens [start, start+count) go to an int32 array or values.
+struct Section {
+  int64_t start, count;
+  int32_t *ints;  // or nullptr -> values
+};
+
+// Parses all tokens of [body, end) in parallel into the given sections.
+// Returns number of tokens seen, or -1 on a malformed token.
+int64_t parse_body(const char *body, const char *end, const std::vector<Section> &secs,
+                   void *vals, int dtype) {
+  const int T = num_threads();
+  const size_t len = (size_t)(end - body);
+  std::vector<const char *> cut(T + 1);
+  cut[0] = body;
+  cut[T] = end;
+  for (int t = 1; t < T; ++t) {
+    const char *p = body + len * t / T;
+    if (p < cut[t - 1]) p = cut[t - 1];
+    while (p < end && !is_space(*p)) ++p;  // move to a token boundary
+    cut[t] = p;
+  }
+  std::vector<int64_t> counts(T, 0);
+  auto count_fn = [&](int t) {
+    int64_t c = 0;
+    const char *p = cut[t], *e = cut[t + 1];
+    bool in_tok = false;
+    for (; p < e; ++p) {
+      const bool sp = is_space(*p);
+      if (!sp && !in_tok) ++c;
+      in_tok = !sp;
+    }
+    counts[t] = c;
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(count_fn, t);
+    for (auto &x : th) x.join();
+  }
+  std::vector<int64_t> first(T + 1, 0);
+  for (int t = 0; t < T; ++t) first[t + 1] = first[t] + counts[t];
+  std::vector<int> bad(T, 0);
+  auto parse_fn = [&](int t) {
+    int64_t idx = first[t];
+    const char *p = cut[t], *e = cut[t + 1];
+    size_t sec = 0;
+    while (true) {
+      while (p < e && is_space(*p)) ++p;
+      if (p >= e) break;
+      while (sec < secs.size() && idx >= secs[sec].start + secs[sec].count) ++sec;
+      const char *tok_end = p;
+      while (tok_end < e && !is_space(*tok_end)) ++tok_end;
+      if (sec < secs.size()) {
+        const Section &s = secs[sec];
+        const int64_t off = idx - s.start;
+        if (s.ints) {
+          long long v = 0;
+          auto r = std::from_chars(p, tok_end, v);
+          if (r.ec != std::errc() || r.ptr != tok_end) { bad[t] = 1; return; }
+          s.ints[off] = (int32_t)v;
+        } else if (dtype == HSPMV_F64) {
+          double v = 0;
+          auto r = std::from_chars(p, tok_end, v);
+          if (r.ec != std::errc() && r.ec != std::errc::result_out_of_range) { bad[t] = 1; return; }
+          ((double *)vals)[off] = v;
+        } else {
+          float v = 0;
+          auto r = std::from_chars(p, tok_end, v);
+          if (r.ec != std::errc() && r.ec != std::errc::result_out_of_range) { bad[t] = 1; return; }
+          ((float *)vals)[off] = v;
+        }
+      }
+      ++idx;
+      p = tok_end;
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(parse_fn, t);
+    for (auto &x : th) x.join();
+  }
+  for (int t = 0; t < T; ++t)
+    if (bad[t]) return -1;
+  return first[T];
+}
+
+void *alloc_vals(int64_t nnz, int dtype) {
+  return malloc((size_t)(nnz ? nnz : 1) * dtype_size(dtype));
+}
+
+}  // namespace
+}  // namespace hspmv
+
+using namespace hspmv;
+
+extern "C" {
+
+const char *hspmv_last_error(void) { return g_err.c_str(); }
+
+const char *hspmv_version(void) { return "hspmv 0.1 (gfx950)"; }
+
+void hspmv_free_csr(hspmv_csr_buf *A) {
+  if (!A) return;
+  free(A->row_ptr);
+  free(A->col_idx);
+  free(A->val);
+  memset(A, 0, sizeof(*A));
+}
+
+void hspmv_free_csr3(hspmv_csr3_buf *mp) {
+  if (!mp) return;
+  free(mp->outer);
+  free(mp->inner);
+  memset(mp, 0, sizeof(*mp));
+}
+
+int hspmv_read_csr(const char *path, int dtype, hspmv_csr_buf *out) {
+  clear_error();
+  if (!path || !out) return set_error(HSPMV_E_INVALID, "NULL argument");
+  if (dtype != HSPMV_F32 && dtype != HSPMV_F64) return set_error(HSPMV_E_INVALID, "bad dtype");
+  memset(out, 0, sizeof(*out));
+  FileBuf fb = slurp(path);
+  if (!fb.ok) return set_error(HSPMV_E_IO, "cannot open %s: %s", path, strerror(errno));
+  const char *beg = fb.data.data(), *end = beg + fb.data.size() - 1;
+  long long h[3];
+  const char *body = parse_header(beg, end, h, 3);
+  if (!body || h[0] < 0 || h[1] < 0 || h[2] < 0)
+    return set_error(HSPMV_E_IO, "%s: malformed header (expected \"m n nnz\")", path);
+  if (h[0] >= INT32_MAX || h[2] >= INT32_MAX)
+    return set_error(HSPMV_E_INVALID, "%s: too large for int32 indices", path);
+  const int64_t m = h[0], n = h[1], nnz = h[2];
+  int32_t *rp = (int32_t *)malloc(sizeof(int32_t) * (size_t)(m + 1));
+  int32_t *ci = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nnz ? nnz : 1));
+  void *val = alloc_vals(nnz, dtype);
+  if (!rp || !ci || !val) {
+    free(rp); free(ci); free(val);
+    return set_error(HSPMV_E_NOMEM, "out of host memory reading %s", path);
+  }
+  std::vector<Section> secs = {{0, m + 1, rp}, {m + 1, nnz, ci}, {m + 1 + nnz, nnz, nullptr}};
+  const int64_t ntok = parse_body(body, end, secs, val, dtype);
+  if (ntok < 0 || ntok < m + 1 + 2 * nnz) {
+    free(rp); free(ci); free(val);
+    return set_error(HSPMV_E_IO, "%s: expected %lld tokens after the header, found %lld",
+                     path, (long long)(m + 1 + 2 * nnz), (long long)ntok);
+  }
+  const int base = rp[0];
+  if (base != 0 && base != 1) {
+    free(rp); free(ci); free(val);
+    return set_error(HSPMV_E_IO, "%s: row_ptr[0] = %d, expected 0 or 1", path, base);
+  }
+  if (base == 1) {
+    for (int64_t i = 0; i <= m; ++i) rp[i] -= 1;
+    for (int64_t k = 0; k < nnz; ++k) ci[k] -= 1;
+  }
+  out->m = m; out->n = n; out->nnz = nnz;
+  out->row_ptr = rp; out->col_idx = ci; out->val = val;
+  out->dtype = dtype; out->index_base = base;
+  hspmv_csr view = {m, n, nnz, rp, ci, val, dtype};
+  int rc = validate_host_csr(&view, true);
+  if (rc != HSPMV_OK) {
+    hspmv_free_csr(out);
+    return rc;
+  }
+  return HSPMV_OK;
+}
+
+int hspmv_read_csr3(const char *path, int dtype, hspmv_csr_buf *A, hspmv_csr3_buf *mp) {
+  clear_error();
+  if (!path || !A || !mp) return set_error(HSPMV_E_INVALID, "NULL argument");
+  if (dtype != HSPMV_F32 && dtype != HSPMV_F64) return set_error(HSPMV_E_INVALID, "bad dtype");
+  memset(A, 0, sizeof(*A));
+  memset(mp, 0, sizeof(*mp));
+  FileBuf fb = slurp(path);
+  if (!fb.ok) return set_error(HSPMV_E_IO, "cannot open %s: %s", path, strerror(errno));
+  const char *beg = fb.data.data(), *end = beg + fb.data.size() - 1;
+  long long h[5];
+  const char *body = parse_header(beg, end, h, 5);
+  if (!body || h[0] < 0 || h[1] < 0 || h[2] < 0 || h[3] < 0 || h[4] < 0)
+    return set_error(HSPMV_E_IO, "%s: malformed header (expected \"nSSR nSR M N NNZ\")", path);
+  if (h[2] >= INT32_MAX || h[4] >= INT32_MAX)
+    return set_error(HSPMV_E_INVALID, "%s: too large for int32 indices", path);
+  const int64_t nssr = h[0], nsr = h[1], m = h[2], n = h[3], nnz = h[4];
+  int32_t *outer = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nssr + 1));
+  int32_t *inner = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nsr + 1));
+  int32_t *rp = (int32_t *)malloc(sizeof(int32_t) * (size_t)(m + 1));
+  int32_t *ci = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nnz ? nnz : 1));
+  void *val = alloc_vals(nnz, dtype);
+  if (!outer || !inner || !rp || !ci || !val) {
+    free(outer); free(inner); free(rp); free(ci); free(val);
+    return set_error(HSPMV_E_NOMEM, "out of host memory reading %s", path);
+  }
+  int64_t o = 0;
+  std::vector<Section> secs;
+  secs.push_back({o, nssr + 1, outer}); o += nssr + 1;
+  secs.push_back({o, nsr + 1, inner}); o += nsr + 1;
+  secs.push_back({o, m + 1, rp}); o += m + 1;
+  secs.push_back({o, nnz, ci}); o += nnz;
+  secs.push_back({o, nnz, nullptr}); o += nnz;
+  const int64_t ntok = parse_body(body, end, secs, val, dtype);
+  if (ntok < 0 || ntok < o) {
+    free(outer); free(inner); free(rp); free(ci); free(val);
+    return set_error(HSPMV_E_IO, "%s: expected %lld tokens after the header, found %lld",
+                     path, (long long)o, (long long)ntok);
+  }
+  A->m = m; A->n = n; A->nnz = nnz; A->row_ptr = rp; A->col_idx = ci; A->val = val;
+  A->dtype = dtype; A->index_base = 0;
+  mp->n_ssr = nssr; mp->n_sr = nsr; mp->outer = outer; mp->inner = inner;
+  hspmv_csr view = {m, n, nnz, rp, ci, val, dtype};
+  int rc = validate_host_csr(&view, true);
+  if (rc == HSPMV_OK) {
+    hspmv_csr3_maps mv = {nssr, nsr, outer, inner};
+    rc = validate_host_maps(&mv, m);
+  }
+  if (rc != HSPMV_OK) {
+    hspmv_free_csr(A);
+    hspmv_free_csr3(mp);
+  }
+  return rc;
+}
+
+// ------------------------------------------------------------ writers
+
+static void write_ints(FILE *fp, const int32_t *a, int64_t cnt) {
+  char buf[1 << 16];
+  size_t pos = 0;
+  for (int64_t i = 0; i < cnt; ++i) {
+    if (pos + 16 > sizeof(buf)) { fwrite(buf, 1, pos, fp); pos = 0; }
+    auto r = std::to_chars(buf + pos, buf + sizeof(buf), a[i]);
+    pos = (size_t)(r.ptr - buf);
+    buf[pos++] = ' ';
+  }
+  fwrite(buf, 1, pos, fp);
+}
+
+static void write_vals(FILE *fp, const void *v, int dtype, int64_t cnt) {
+  for (int64_t i = 0; i < cnt; ++i) {
+    const double d = dtype == HSPMV_F64 ? ((const double *)v)[i] : (double)((const float *)v)[i];
+    fprintf(fp, "%f ", d);
+  }
+}
+
+int hspmv_write_csr(const char *path, const hspmv_csr *A) {
+  clear_error();
+  int rc = validate_host_csr(A, false);
+  if (rc) return rc;
+  FILE *fp = fopen(path, "w");
+  if (!fp) return set_error(HSPMV_E_IO, "cannot create %s: %s", path, strerror(errno));
+  // helpers/converter.m:25-33: "%d %d %d\n", then "%d " row_ptr, "%d " col_ind,
+  // "%f " val, each line ending " \n".
+  fprintf(fp, "%lld %lld %lld\n", (long long)A->m, (long long)A->n, (long long)A->nnz);
+  write_ints(fp, A->row_ptr, A->m + 1);
+  fputc('\n', fp);
+  write_ints(fp, A->col_idx, A->nnz);
+  fputc('\n', fp);
+  write_vals(fp, A->val, A->dtype, A->nnz);
+  fputc('\n', fp);
+  if (fclose(fp) != 0) return set_error(HSPMV_E_IO, "write failed for %s", path);
+  return HSPMV_OK;
+}
+
+int hspmv_write_csr3(const char *path, const hspmv_csr *A, const hspmv_csr3_maps *mp) {
+  clear_error();
+  int rc = validate_host_csr(A, false);
+  if (rc) return rc;
+  if (!mp) return set_error(HSPMV_E_INVALID, "maps are NULL");
+  rc = validate_host_maps(mp, A->m);
+  if (rc) return rc;
+  FILE *fp = fopen(path, "w");
+  if (!fp) return set_error(HSPMV_E_IO, "cannot create %s: %s", path, strerror(errno));
+  // reformat-csr-to-csr3/spmv-auto.cpp:38-62: "%ld %ld %ld %ld %ld \n" then
+  // every array "%u " on one stream, values "%.6f ".
+  fprintf(fp, "%lld %lld %lld %lld %lld \n", (long long)mp->n_ssr, (long long)mp->n_sr,
+          (long long)A->m, (long long)A->n, (long long)A->nnz);
+  write_ints(fp, mp->outer, mp->n_ssr + 1);
+  write_ints(fp, mp->inner, mp->n_sr + 1);
+  write_ints(fp, A->row_ptr, A->m + 1);
+  write_ints(fp, A->col_idx, A->nnz);
+  for (int64_t i = 0; i < A->nnz; ++i) {
+    const double d = A->dtype == HSPMV_F64 ? ((const double *)A->val)[i]
+                                           : (double)((const float *)A->val)[i];
+    fprintf(fp, "%.6f ", d);
+  }
+  if (fclose(fp) != 0) return set_error(HSPMV_E_IO, "write failed for %s", path);
+  return HSPMV_OK;
+}
+
+// ------------------------------------------------------------ binary cache
+// Layout: "HSPMVBIN" magic, u32 version=1, i32 dtype, i64 m, n, nnz, n_ssr,
+// n_sr, then row_ptr[m+1], col[nnz], val[nnz], outer[n_ssr+1], inner[n_sr+1]
+// (maps only when n_ssr > 0).
+
+static const char kMagic[8] = {'H', 'S', 'P', 'M', 'V', 'B', 'I', 'N'};
+
+int hspmv_save_bin(const char *path, const hspmv_csr *A, const hspmv_csr3_maps *mp) {
+  clear_error();
+  int rc = validate_host_csr(A, false);
+  if (rc) return rc;
+  if (mp && (rc = validate_host_maps(mp, A->m))) return rc;
+  FILE *fp = fopen(path, "wb");
+  if (!fp) return set_error(HSPMV_E_IO, "cannot create %s: %s", path, strerror(errno));
+  uint32_t ver = 1;
+  int32_t dt = A->dtype;
+  int64_t hdr[5] = {A->m, A->n, A->nnz, mp ? mp->n_ssr : 0, mp ? mp->n_sr : 0};
+  bool ok = fwrite(kMagic, 1, 8, fp) == 8 && fwrite(&ver, 4, 1, fp) == 1 &&
+            fwrite(&dt, 4, 1, fp) == 1 && fwrite(hdr, 8, 5, fp) == 5;
+  ok = ok && fwrite(A->row_ptr, 4, (size_t)(A->m + 1), fp) == (size_t)(A->m + 1);
+  ok = ok && (A->nnz == 0 || fwrite(A->col_idx, 4, (size_t)A->nnz, fp) == (size_t)A->nnz);
+  ok = ok && (A->nnz == 0 ||
+              fwrite(A->val, dtype_size(A->dtype), (size_t)A->nnz, fp) == (size_t)A->nnz);
+  if (mp && mp->n_ssr > 0) {
+    ok = ok && fwrite(mp->outer, 4, (size_t)(mp->n_ssr + 1), fp) == (size_t)(mp->n_ssr + 1);
+    ok = ok && fwrite(mp->inner, 4, (size_t)(mp->n_sr + 1), fp) == (size_t)(mp->n_sr + 1);
+  }
+  if (fclose(fp) != 0) ok = false;
+  return ok ? HSPMV_OK : set_error(HSPMV_E_IO, "write failed for %s", path);
+}
+
+int hspmv_load_bin(const char *path, hspmv_csr_buf *A, hspmv_csr3_buf *mp) {
+  clear_error();
+  if (!path || !A) return set_error(HSPMV_E_INVALID, "NULL argument");
+  memset(A, 0, sizeof(*A));
+  if (mp) memset(mp, 0, sizeof(*mp));
+  FILE *fp = fopen(path, "rb");
+  if (!fp) return set_error(HSPMV_E_IO, "cannot open %s: %s", path, strerror(errno));
+  char magic[8];
+  uint32_t ver = 0;
+  int32_t dt = 0;
+  int64_t hdr[5];
+  if (fread(magic, 1, 8, fp) != 8 || memcmp(magic, kMagic, 8) != 0 || fread(&ver, 4, 1, fp) != 1 ||
+      ver != 1 || fread(&dt, 4, 1, fp) != 1 || fread(hdr, 8, 5, fp) != 5 ||
+      (dt != HSPMV_F32 && dt != HSPMV_F64) || hdr[0] < 0 || hdr[2] < 0 || hdr[3] < 0 ||
+      hdr[4] < 0 || hdr[0] >= INT32_MAX || hdr[2] >= INT32_MAX) {
+    fclose(fp);
+    return set_error(HSPMV_E_IO, "%s: not an hspmv binary cache", path);
+  }
+  const int64_t m = hdr[0], nnz = hdr[2], nssr = hdr[3], nsr = hdr[4];
+  A->m = m; A->n = hdr[1]; A->nnz = nnz; A->dtype = dt; A->index_base = 0;
+  A->row_ptr = (int32_t *)malloc(4 * (size_t)(m + 1));
+  A->col_idx = (int32_t *)malloc(4 * (size_t)(nnz ? nnz : 1));
+  A->val = alloc_vals(nnz, dt);
+  bool ok = A->row_ptr && A->col_idx && A->val;
+  ok = ok && fread(A->row_ptr, 4, (size_t)(m + 1), fp) == (size_t)(m + 1);
+  ok = ok && (nnz == 0 || fread(A->col_idx, 4, (size_t)nnz, fp) == (size_t)nnz);
+  ok = ok && (nnz == 0 || fread(A->val, dtype_size(dt), (size_t)nnz, fp) == (size_t)nnz);
+  if (ok && nssr > 0 && mp) {
+    mp->n_ssr = nssr; mp->n_sr = nsr;
+    mp->outer = (int32_t *)malloc(4 * (size_t)(nssr + 1));
+    mp->inner = (int32_t *)malloc(4 * (size_t)(nsr + 1));
+    ok = mp->outer && mp->inner &&
+         fread(mp->outer, 4, (size_t)(nssr + 1), fp) == (size_t)(nssr + 1) &&
+         fread(mp->inner, 4, (size_t)(nsr + 1), fp) == (size_t)(nsr + 1);
+  }
+  fclose(fp);
+  if (!ok) {
+    hspmv_free_csr(A);
+    if (mp) hspmv_free_csr3(mp);
+    return set_error(HSPMV_E_IO, "%s: truncated binary cache", path);
+  }
+  hspmv_csr view = {A->m, A->n, A->nnz, A->row_ptr, A->col_idx, A->val, A->dtype};
+  int rc = validate_host_csr(&view, true);
+  if (rc == HSPMV_OK && mp && mp->n_ssr > 0) {
+    hspmv_csr3_maps mv = {mp->n_ssr, mp->n_sr, mp->outer, mp->inner};
+    rc = validate_host_maps(&mv, m);
+  }
+  if (rc != HSPMV_OK) {
+    hspmv_free_csr(A);
+    if (mp) hspmv_free_csr3(mp);
+  }
+  return rc;
+}
+
+// ------------------------------------------------------------ CSR-3 maps
+// Grouping rule of BAND_k::handCoarsen (cuda-spmv-csrk/hip/csrk.cu:1450-1484):
+// a group absorbs consecutive vertices while its running nnz count is below
+// the threshold, so every group but the last holds >= threshold nonzeros.
+
+// The open group is closed whenever it holds rows (the reference closes it
+// only when it holds nonzeros, csrk.cu:1481-1484, which leaves a trailing run
+// of empty rows unmapped); identical maps on every other matrix.
+static int64_t group_by_threshold(int64_t N, const std::vector<int64_t> &deg, int64_t thr,
+                                  std::vector<int32_t> *starts) {
+  int64_t ng = 0, acc = 0, last = 0;
+  if (starts) starts->assign(1, 0);
+  for (int64_t i = 0; i < N; ++i) {
+    if (acc < thr) {
+      acc += deg[i];
+    } else {
+      ++ng;
+      acc = deg[i];
+      last = i;
+      if (starts) starts->push_back((int32_t)i);
+    }
+  }
+  if (N > last) {
+    ++ng;
+    if (starts) starts->push_back((int32_t)N);
+  }
+  return ng;
+}
+
+int hspmv_build_csr3_maps(const hspmv_csr *A, int ssrs, int srs, hspmv_csr3_buf *out) {
+  clear_error();
+  if (!out) return set_error(HSPMV_E_INVALID, "NULL output");
+  memset(out, 0, sizeof(*out));
+  int rc = validate_host_csr(A, true);
+  if (rc) return rc;
+  if (ssrs < 1 || srs < 1) return set_error(HSPMV_E_INVALID, "ssrs/srs must be >= 1");
+  const int64_t m = A->m, nnz = A->nnz;
+  std::vector<int64_t> deg((size_t)m);
+  for (int64_t i = 0; i < m; ++i) deg[i] = A->row_ptr[i + 1] - A->row_ptr[i];
+  // level 1 threshold: supRowSizes[0] * NNZ / N (csrk.cu:1089-1091, int)
+  const int64_t thr1 = (int64_t)(int)((int64_t)ssrs * nnz / (m ? m : 1));
+  std::vector<int32_t> inner;
+  const int64_t n1 = group_by_threshold(m, deg, thr1, &inner);
+  if (n1 == 0) inner.assign(1, 0);
+  // Level-1 coarse graph degrees (distinct symmetrised super-row neighbours,
+  // csrk.cu:1487-1610) give NNZ_1 for the level-2 threshold.
+  std::vector<int32_t> sup((size_t)m);
+  for (int64_t s = 0; s < n1; ++s)
+    for (int32_t r = inner[s]; r < inner[s + 1]; ++r) sup[r] = (int32_t)s;
+  std::vector<std::vector<int32_t>> adj((size_t)n1);
+  for (int64_t s = 0; s < n1; ++s)
+    for (int32_t r = inner[s]; r < inner[s + 1]; ++r)
+      for (int32_t k = A->row_ptr[r]; k < A->row_ptr[r + 1]; ++k) {
+        const int32_t c = A->col_idx[k];
+        if (c >= inner[s] && c < m) {
+          const int32_t t = sup[c];
+          adj[s].push_back(t);
+          if (t != s) adj[t].push_back((int32_t)s);
+        }
+      }
+  std::vector<int64_t> deg1((size_t)n1);
+  int64_t nnz1 = 0;
+  for (int64_t s = 0; s < n1; ++s) {
+    auto &a = adj[s];
+    std::sort(a.begin(), a.end());
+    deg1[s] = (int64_t)(std::unique(a.begin(), a.end()) - a.begin());
+    nnz1 += deg1[s];
+    std::vector<int32_t>().swap(a);
+  }
+  const int64_t thr2 = (int64_t)(int)((int64_t)srs * nnz1 / (n1 ? n1 : 1));
+  std::vector<int32_t> outer;
+  const int64_t n2 = group_by_threshold(n1, deg1, thr2, &outer);
+  if (n2 == 0) outer.assign(1, 0);
+  out->n_ssr = n2;
+  out->n_sr = n1;
+  out->outer = (int32_t *)malloc(4 * (size_t)(n2 + 1));
+  out->inner = (int32_t *)malloc(4 * (size_t)(n1 + 1));
+  if (!out->outer || !out->inner) {
+    hspmv_free_csr3(out);
+    return set_error(HSPMV_E_NOMEM, "out of host memory");
+  }
+  memcpy(out->outer, outer.data(), 4 * (size_t)(n2 + 1));
+  memcpy(out->inner, inner.data(), 4 * (size_t)(n1 + 1));
+  return HSPMV_OK;
+}
+
+int hspmv_csr3_params(double d, int flavour, int *ssrs_out, int *srs_out) {
+  clear_error();
+  if (!ssrs_out || !srs_out || !(d > 0.0)) return set_error(HSPMV_E_INVALID, "bad arguments");
+  int ssrs, srs;
+  if (flavour == 0) {
+    // reformat-csr-to-csr3/spmv-auto.cpp:154-173 (== cuda/spmv-auto-volta.cu)
+    ssrs = (int)std::floor(8.89888 - 1.25 * std::log(d) + 0.5);
+    srs = (int)std::floor(10.14618 - 1.5 * std::log(d) + 0.5);
+    if (d > 8.0 && d <= 16.0) {
+      ssrs = (int)std::floor((double)ssrs * 1.5 + 0.5);
+      srs = ssrs * 2;
+    } else if (d > 16.0 && d <= 32.0) {
+      ssrs *= 4;
+      srs = ssrs >> 1;
+    } else if (d > 32.0) {
+      ssrs *= 5;
+      srs = ssrs >> 1;
+    }
+  } else if (flavour == 1) {
+    // cuda-spmv-csrk/hip/spmv-auto-mi100.cu:130-158
+    ssrs = (int)std::floor(0.5 + (8.489 - 1.15 * std::log(d)));
+    srs = (int)std::floor(0.5 + (10.711 - 1.607 * std::log(d)));
+    if (d > 8.0 && d <= 16.0) {
+      srs = ssrs * 4;
+    } else if (d > 16.0 && d <= 32.0) {
+      ssrs = (int)std::floor((double)ssrs * 2.5 + 0.5);
+      srs = ssrs * 3;
+    } else if (d > 32.0 && d <= 64.0) {
+      ssrs *= 2;
+      srs = ssrs * 2;
+    } else if (d > 64.0) {
+      ssrs = (int)std::floor((double)ssrs * 2.7 + 0.5);
+      srs = (int)std::floor((double)ssrs / 4 + 0.5);
+    }
+  } else {
+    // MI355X: a super-row ~ one wave task (64 rows of average length),
+    // a super-super-row ~ 4 such tasks (one 256-thread workgroup).
+    ssrs = 64;
+    srs = 4;
+  }
+  *ssrs_out = ssrs < 1 ? 1 : ssrs;
+  *srs_out = srs < 1 ? 1 : srs;
+  return HSPMV_OK;
+}
+
+// ------------------------------------------------------------ misc
+
+int hspmv_partition_rows(int64_t m, const int32_t *rp, const hspmv_csr3_maps *mp, int parts,
+                         int64_t *splits) {
+  clear_error();
+  if (!rp || !splits || parts < 1 || m < 0) return set_error(HSPMV_E_INVALID, "bad arguments");
+  const int64_t nnz = rp[m];
+  splits[0] = 0;
+  splits[parts] = m;
+  if (mp && mp->n_ssr > 0) {
+    // split on super-super-row boundaries
+    const int64_t nssr = mp->n_ssr;
+    int64_t s = 0;
+    for (int p = 1; p < parts; ++p) {
+      const int64_t target = nnz * p / parts;
+      while (s < nssr && rp[mp->inner[mp->outer[s]]] < target) ++s;
+      splits[p] = mp->inner[mp->outer[s]];
+    }
+  } else {
+    for (int p = 1; p < parts; ++p) {
+      const int64_t target = nnz * p / parts;
+      // first row r with rp[r] >= target
+      int64_t lo = 0, hi = m;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        if (rp[mid] < target) lo = mid + 1; else hi = mid;
+      }
+      splits[p] = lo;
+    }
+  }
+  for (int p = 1; p <= parts; ++p)
+    if (splits[p] < splits[p - 1]) splits[p] = splits[p - 1];
+  return HSPMV_OK;
+}
+
+double hspmv_alg_bytes(int64_t m, int64_t n, int64_t nnz, int dtype, int64_t n_ssr, int64_t n_sr) {
+  const double sv = (double)dtype_size(dtype), si = 4.0;
+  double b = (double)nnz * (sv + si) + (double)(m + 1) * si + (double)n * sv + (double)m * sv;
+  if (n_ssr > 0) b += (double)(n_ssr + 1 + n_sr + 1) * si;
+  return b;
+}
+
+}  // extern "C"

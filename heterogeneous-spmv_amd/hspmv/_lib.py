@@ -1,0 +1,137 @@
+"""ctypes binding of libhspmv.so (the C ABI declared in include/hspmv.h).
+
+The library is loaded from ``heterogeneous-spmv_amd/build/libhspmv.so`` (built
+in-tree by ``make`` / ``__graft_entry__.build()``).  There is no fallback: if
+the shared library is missing or fails to load, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parent.parent          # heterogeneous-spmv_amd/
+REPO_ROOT = PKG_ROOT.parent
+LIB_PATH = Path(os.environ.get("HSPMV_LIB", PKG_ROOT / "build" / "libhspmv.so"))
+HEADER = REPO_ROOT / "include" / "hspmv.h"
+
+F32, F64 = 0, 1
+
+KERNEL_AUTO, KERNEL_VECTOR, KERNEL_STREAM, KERNEL_CSR3 = 0, 1, 2, 3
+LANES_SHIFT = 4
+FLAG_NONTEMPORAL = 1 << 12
+FLAG_DEVICE_PTRS = 1 << 13
+
+E_CODES = {0: "OK", -1: "E_INVALID", -2: "E_IO", -3: "E_NOMEM", -4: "E_HIP",
+           -5: "E_RCCL", -6: "E_NODEV", -7: "E_STATE"}
+
+
+def lanes_flag(lanes: int) -> int:
+    return (int(lanes) & 0x7F) << LANES_SHIFT
+
+
+class HspmvError(RuntimeError):
+    def __init__(self, what: str, code: int, msg: str):
+        super().__init__(f"{what}: {E_CODES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Csr(C.Structure):
+    _fields_ = [("m", C.c_int64), ("n", C.c_int64), ("nnz", C.c_int64),
+                ("row_ptr", C.c_void_p), ("col_idx", C.c_void_p), ("val", C.c_void_p),
+                ("dtype", C.c_int32)]
+
+
+class Csr3Maps(C.Structure):
+    _fields_ = [("n_ssr", C.c_int64), ("n_sr", C.c_int64),
+                ("outer", C.c_void_p), ("inner", C.c_void_p)]
+
+
+class CsrBuf(C.Structure):
+    _fields_ = [("m", C.c_int64), ("n", C.c_int64), ("nnz", C.c_int64),
+                ("row_ptr", C.c_void_p), ("col_idx", C.c_void_p), ("val", C.c_void_p),
+                ("dtype", C.c_int32), ("index_base", C.c_int32)]
+
+
+class Csr3Buf(C.Structure):
+    _fields_ = [("n_ssr", C.c_int64), ("n_sr", C.c_int64),
+                ("outer", C.c_void_p), ("inner", C.c_void_p)]
+
+
+class Timing(C.Structure):
+    _fields_ = [("t_min", C.c_double), ("t_max", C.c_double), ("t_avg", C.c_double),
+                ("wall_min", C.c_double), ("wall_max", C.c_double), ("wall_avg", C.c_double),
+                ("gflops", C.c_double), ("gbps_alg", C.c_double),
+                ("iters", C.c_int32), ("num_gpus", C.c_int32)]
+
+
+class Info(C.Structure):
+    _fields_ = [("kernel", C.c_int32), ("lanes", C.c_int32), ("waves_per_block", C.c_int32),
+                ("num_gpus", C.c_int32), ("blocks", C.c_int64), ("alg_bytes", C.c_double),
+                ("flops", C.c_double), ("device_bytes", C.c_int64)]
+
+
+_P = C.c_void_p
+_H = C.c_void_p
+# name -> (restype, argtypes); every entry point declared in include/hspmv.h
+SIGNATURES = {
+    "hspmv_create": (C.c_int, [C.POINTER(_H), C.POINTER(Csr), C.POINTER(Csr3Maps), C.c_int, C.c_uint]),
+    "hspmv_create_on_device": (C.c_int, [C.POINTER(_H), C.POINTER(Csr), C.POINTER(Csr3Maps),
+                                         C.c_int, _P, C.c_uint]),
+    "hspmv_set_x": (C.c_int, [_H, _P]),
+    "hspmv_bind_x_device": (C.c_int, [_H, _P]),
+    "hspmv_bind_y_device": (C.c_int, [_H, _P]),
+    "hspmv_x_device": (_P, [_H, C.c_int]),
+    "hspmv_y_device": (_P, [_H, C.c_int]),
+    "hspmv_spmv": (C.c_int, [_H]),
+    "hspmv_synchronize": (C.c_int, [_H]),
+    "hspmv_run": (C.c_int, [_H, C.c_int, C.c_int, C.POINTER(Timing)]),
+    "hspmv_get_y": (C.c_int, [_H, _P]),
+    "hspmv_exchange": (C.c_int, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "hspmv_get_info": (C.c_int, [_H, C.POINTER(Info)]),
+    "hspmv_destroy": (None, [_H]),
+    "hspmv_read_csr": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(CsrBuf)]),
+    "hspmv_read_csr3": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(CsrBuf), C.POINTER(Csr3Buf)]),
+    "hspmv_write_csr": (C.c_int, [C.c_char_p, C.POINTER(Csr)]),
+    "hspmv_write_csr3": (C.c_int, [C.c_char_p, C.POINTER(Csr), C.POINTER(Csr3Maps)]),
+    "hspmv_save_bin": (C.c_int, [C.c_char_p, C.POINTER(Csr), C.POINTER(Csr3Maps)]),
+    "hspmv_load_bin": (C.c_int, [C.c_char_p, C.POINTER(CsrBuf), C.POINTER(Csr3Buf)]),
+    "hspmv_free_csr": (None, [C.POINTER(CsrBuf)]),
+    "hspmv_free_csr3": (None, [C.POINTER(Csr3Buf)]),
+    "hspmv_build_csr3_maps": (C.c_int, [C.POINTER(Csr), C.c_int, C.c_int, C.POINTER(Csr3Buf)]),
+    "hspmv_csr3_params": (C.c_int, [C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "hspmv_partition_rows": (C.c_int, [C.c_int64, _P, C.POINTER(Csr3Maps), C.c_int, _P]),
+    "hspmv_alg_bytes": (C.c_double, [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int64]),
+    "hspmv_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "hspmv_last_error": (C.c_char_p, []),
+    "hspmv_version": (C.c_char_p, []),
+}
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    """Loads libhspmv.so once (RTLD_GLOBAL off).  Raises if it is missing."""
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"libhspmv.so not found at {LIB_PATH}: build it with "
+                f"`make -C {PKG_ROOT}` or `python -c 'import __graft_entry__ as g; g.build()'`")
+        handle = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = handle
+    return _LIB
+
+
+def last_error() -> str:
+    msg = lib().hspmv_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise HspmvError(what, rc, last_error())

@@ -1,0 +1,330 @@
+"""Python host mirror of the reference's CSR / CSR-3 SpMV interface, on top of
+the libhspmv C ABI (include/hspmv.h).
+
+Reference interface it mirrors:
+
+* ``CSRk_Graph(nRows, nCols, nnz, rVec, cVec, val, ..., k, supRowSizes)`` +
+  ``putInCSRkFormat()`` / ``setX()`` / ``setY()`` / ``getY()``
+  (cuda-spmv-csrk/hip/csrk.cuh:321-353)  ->  :class:`SpMV` (+ :func:`build_csr3_maps`)
+* ``my_read_csr`` (spmv-csr/spmv.c:11-57), ``my_read_csr3``
+  (reformat-csr-to-csr3/stats.c:10-79)  ->  :func:`read_csr`, :func:`read_csr3`
+* the timed loop + ``TimeMin/TimeMax/TimeAvg`` (spmv-csr/spmv.c:164-185)
+  ->  :meth:`SpMV.run`
+
+Every call goes to the GPU through libhspmv; errors raise :class:`HspmvError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import (F32, F64, KERNEL_AUTO, KERNEL_CSR3, KERNEL_STREAM, KERNEL_VECTOR,
+                   FLAG_DEVICE_PTRS, FLAG_NONTEMPORAL, HspmvError, check, lanes_flag, lib)
+
+_KERNELS = {"auto": KERNEL_AUTO, "vector": KERNEL_VECTOR, "stream": KERNEL_STREAM,
+            "csr3": KERNEL_CSR3}
+KERNEL_NAMES = {v: k for k, v in _KERNELS.items()}
+
+
+def dtype_code(dtype) -> int:
+    dt = np.dtype(dtype)
+    if dt == np.float64:
+        return F64
+    if dt == np.float32:
+        return F32
+    raise ValueError(f"unsupported dtype {dt} (float32 / float64)")
+
+
+def np_dtype(code: int):
+    return np.float64 if code == F64 else np.float32
+
+
+def _ptr(a: Optional[np.ndarray]) -> Optional[int]:
+    return None if a is None else a.ctypes.data
+
+
+@dataclass
+class CsrMatrix:
+    """Host CSR matrix (0-based int32 indices, float32/float64 values)."""
+    m: int
+    n: int
+    row_ptr: np.ndarray
+    col_idx: np.ndarray
+    val: np.ndarray
+    index_base: int = 0
+
+    def __post_init__(self):
+        self.row_ptr = np.ascontiguousarray(self.row_ptr, dtype=np.int32)
+        self.col_idx = np.ascontiguousarray(self.col_idx, dtype=np.int32)
+        self.val = np.ascontiguousarray(self.val)
+        if self.val.dtype not in (np.float32, np.float64):
+            self.val = self.val.astype(np.float64)
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col_idx.shape[0])
+
+    @property
+    def dtype(self):
+        return self.val.dtype
+
+    def astype(self, dtype) -> "CsrMatrix":
+        return CsrMatrix(self.m, self.n, self.row_ptr, self.col_idx,
+                         self.val.astype(dtype), self.index_base)
+
+    def c_struct(self) -> _lib.Csr:
+        return _lib.Csr(self.m, self.n, self.nnz, _ptr(self.row_ptr), _ptr(self.col_idx),
+                        _ptr(self.val), dtype_code(self.val.dtype))
+
+    @classmethod
+    def from_scipy(cls, S, dtype=np.float64) -> "CsrMatrix":
+        S = S.tocsr()
+        S.sort_indices()
+        return cls(S.shape[0], S.shape[1], S.indptr, S.indices, S.data.astype(dtype))
+
+    def to_scipy(self):
+        import scipy.sparse as sp
+        return sp.csr_matrix((self.val, self.col_idx, self.row_ptr), shape=(self.m, self.n))
+
+    def rows(self, r0: int, r1: int) -> "CsrMatrix":
+        """Rows [r0, r1) with row_ptr rebased to 0 (global columns kept)."""
+        k0, k1 = int(self.row_ptr[r0]), int(self.row_ptr[r1])
+        return CsrMatrix(r1 - r0, self.n, self.row_ptr[r0:r1 + 1] - k0,
+                         self.col_idx[k0:k1], self.val[k0:k1])
+
+
+@dataclass
+class Csr3Maps:
+    """CSR-3 multilevel maps: outer (n_ssr+1) -> super-rows, inner (n_sr+1) -> rows."""
+    outer: np.ndarray
+    inner: np.ndarray
+
+    def __post_init__(self):
+        self.outer = np.ascontiguousarray(self.outer, dtype=np.int32)
+        self.inner = np.ascontiguousarray(self.inner, dtype=np.int32)
+
+    @property
+    def n_ssr(self) -> int:
+        return int(self.outer.shape[0] - 1)
+
+    @property
+    def n_sr(self) -> int:
+        return int(self.inner.shape[0] - 1)
+
+    def c_struct(self) -> _lib.Csr3Maps:
+        return _lib.Csr3Maps(self.n_ssr, self.n_sr, _ptr(self.outer), _ptr(self.inner))
+
+
+# ------------------------------------------------------------------ formats
+
+def _take_csr(buf: _lib.CsrBuf) -> CsrMatrix:
+    m, nnz = int(buf.m), int(buf.nnz)
+    dt = np_dtype(buf.dtype)
+    rp = np.ctypeslib.as_array(C.cast(buf.row_ptr, C.POINTER(C.c_int32)), (m + 1,)).copy()
+    if nnz:
+        ci = np.ctypeslib.as_array(C.cast(buf.col_idx, C.POINTER(C.c_int32)), (nnz,)).copy()
+        ctype = C.c_double if dt == np.float64 else C.c_float
+        val = np.ctypeslib.as_array(C.cast(buf.val, C.POINTER(ctype)), (nnz,)).copy()
+    else:
+        ci = np.zeros(0, np.int32)
+        val = np.zeros(0, dt)
+    A = CsrMatrix(m, int(buf.n), rp, ci, val, int(buf.index_base))
+    lib().hspmv_free_csr(C.byref(buf))
+    return A
+
+
+def _take_maps(buf: _lib.Csr3Buf) -> Optional[Csr3Maps]:
+    if buf.n_ssr <= 0:
+        lib().hspmv_free_csr3(C.byref(buf))
+        return None
+    o = np.ctypeslib.as_array(C.cast(buf.outer, C.POINTER(C.c_int32)), (int(buf.n_ssr) + 1,)).copy()
+    i = np.ctypeslib.as_array(C.cast(buf.inner, C.POINTER(C.c_int32)), (int(buf.n_sr) + 1,)).copy()
+    lib().hspmv_free_csr3(C.byref(buf))
+    return Csr3Maps(o, i)
+
+
+def read_csr(path: str, dtype=np.float64) -> CsrMatrix:
+    buf = _lib.CsrBuf()
+    check(lib().hspmv_read_csr(str(path).encode(), dtype_code(dtype), C.byref(buf)), "read_csr")
+    return _take_csr(buf)
+
+
+def read_csr3(path: str, dtype=np.float64):
+    buf, mbuf = _lib.CsrBuf(), _lib.Csr3Buf()
+    check(lib().hspmv_read_csr3(str(path).encode(), dtype_code(dtype), C.byref(buf),
+                                C.byref(mbuf)), "read_csr3")
+    return _take_csr(buf), _take_maps(mbuf)
+
+
+def write_csr(path: str, A: CsrMatrix) -> None:
+    cs = A.c_struct()
+    check(lib().hspmv_write_csr(str(path).encode(), C.byref(cs)), "write_csr")
+
+
+def write_csr3(path: str, A: CsrMatrix, maps: Csr3Maps) -> None:
+    cs, ms = A.c_struct(), maps.c_struct()
+    check(lib().hspmv_write_csr3(str(path).encode(), C.byref(cs), C.byref(ms)), "write_csr3")
+
+
+def save_bin(path: str, A: CsrMatrix, maps: Optional[Csr3Maps] = None) -> None:
+    cs = A.c_struct()
+    ms = maps.c_struct() if maps is not None else None
+    check(lib().hspmv_save_bin(str(path).encode(), C.byref(cs),
+                               C.byref(ms) if ms is not None else None), "save_bin")
+
+
+def load_bin(path: str):
+    buf, mbuf = _lib.CsrBuf(), _lib.Csr3Buf()
+    check(lib().hspmv_load_bin(str(path).encode(), C.byref(buf), C.byref(mbuf)), "load_bin")
+    return _take_csr(buf), _take_maps(mbuf)
+
+
+def build_csr3_maps(A: CsrMatrix, ssrs: int, srs: int) -> Csr3Maps:
+    cs, mbuf = A.c_struct(), _lib.Csr3Buf()
+    check(lib().hspmv_build_csr3_maps(C.byref(cs), int(ssrs), int(srs), C.byref(mbuf)),
+          "build_csr3_maps")
+    maps = _take_maps(mbuf)
+    if maps is None:  # empty matrix: one empty super-super-row is not needed
+        maps = Csr3Maps(np.zeros(1, np.int32), np.zeros(1, np.int32))
+    return maps
+
+
+_FLAVOURS = {"volta": 0, "csr3-writer": 0, "mi100": 1, "mi355x": 2}
+
+
+def csr3_params(nnz_per_row: float, flavour: str = "mi355x"):
+    a, b = C.c_int(), C.c_int()
+    check(lib().hspmv_csr3_params(float(nnz_per_row), _FLAVOURS[flavour], C.byref(a), C.byref(b)),
+          "csr3_params")
+    return a.value, b.value
+
+
+def partition_rows(row_ptr: np.ndarray, parts: int, maps: Optional[Csr3Maps] = None) -> np.ndarray:
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int32)
+    out = np.zeros(parts + 1, np.int64)
+    ms = maps.c_struct() if maps is not None else None
+    check(lib().hspmv_partition_rows(rp.shape[0] - 1, _ptr(rp),
+                                     C.byref(ms) if ms is not None else None, int(parts),
+                                     _ptr(out)), "partition_rows")
+    return out
+
+
+def alg_bytes(m: int, n: int, nnz: int, dtype, n_ssr: int = 0, n_sr: int = 0) -> float:
+    return float(lib().hspmv_alg_bytes(m, n, nnz, dtype_code(dtype), n_ssr, n_sr))
+
+
+def device_count() -> int:
+    c = C.c_int()
+    rc = lib().hspmv_device_count(C.byref(c))
+    return c.value if rc == 0 else 0
+
+
+def version() -> str:
+    return lib().hspmv_version().decode()
+
+
+# ------------------------------------------------------------------ handle
+
+class SpMV:
+    """One SpMV operator y = A x on one or more GPUs (a libhspmv handle).
+
+    ``kernel``: "auto" | "stream" | "vector" | "csr3";  ``lanes``: lanes per row
+    for "vector" (0 = auto).  ``device``/``stream``: single-device handle on that
+    HIP device / hipStream_t (as an int); otherwise ``num_gpus`` GPUs with the
+    row-range partition.
+    """
+
+    def __init__(self, A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, num_gpus: int = 1,
+                 kernel: str = "auto", lanes: int = 0, nontemporal: bool = False,
+                 device: Optional[int] = None, stream: Optional[int] = None):
+        self.A = A
+        self.maps = maps
+        self.dtype = A.val.dtype
+        flags = _KERNELS[kernel] | lanes_flag(lanes) | (FLAG_NONTEMPORAL if nontemporal else 0)
+        cs = A.c_struct()
+        ms = maps.c_struct() if maps is not None else None
+        h = C.c_void_p()
+        if device is not None:
+            rc = lib().hspmv_create_on_device(C.byref(h), C.byref(cs),
+                                              C.byref(ms) if ms is not None else None,
+                                              int(device), stream, flags)
+        else:
+            rc = lib().hspmv_create(C.byref(h), C.byref(cs),
+                                    C.byref(ms) if ms is not None else None, int(num_gpus), flags)
+        check(rc, "hspmv_create")
+        self._h = h
+
+    # -- vectors
+    def set_x(self, x: np.ndarray) -> None:
+        x = np.ascontiguousarray(x, dtype=self.dtype)
+        if x.shape[0] != self.A.n:
+            raise ValueError(f"x has {x.shape[0]} entries, expected n={self.A.n}")
+        check(lib().hspmv_set_x(self._h, _ptr(x)), "hspmv_set_x")
+
+    def bind_x_device(self, ptr: Optional[int]) -> None:
+        check(lib().hspmv_bind_x_device(self._h, ptr), "hspmv_bind_x_device")
+
+    def bind_y_device(self, ptr: Optional[int]) -> None:
+        check(lib().hspmv_bind_y_device(self._h, ptr), "hspmv_bind_y_device")
+
+    def x_device(self, gpu: int = 0) -> int:
+        return lib().hspmv_x_device(self._h, gpu) or 0
+
+    def y_device(self, gpu: int = 0) -> int:
+        return lib().hspmv_y_device(self._h, gpu) or 0
+
+    # -- compute
+    def spmv(self) -> None:
+        check(lib().hspmv_spmv(self._h), "hspmv_spmv")
+
+    def synchronize(self) -> None:
+        check(lib().hspmv_synchronize(self._h), "hspmv_synchronize")
+
+    def run(self, warmup: int = 5, iters: int = 20) -> dict:
+        t = _lib.Timing()
+        check(lib().hspmv_run(self._h, int(warmup), int(iters), C.byref(t)), "hspmv_run")
+        return {k: getattr(t, k) for k, _ in _lib.Timing._fields_}
+
+    def get_y(self) -> np.ndarray:
+        y = np.empty(self.A.m, dtype=self.dtype)
+        check(lib().hspmv_get_y(self._h, _ptr(y)), "hspmv_get_y")
+        return y
+
+    def __call__(self, x: np.ndarray) -> np.ndarray:
+        self.set_x(x)
+        self.spmv()
+        return self.get_y()
+
+    def exchange(self):
+        b, g = C.c_double(), C.c_double()
+        check(lib().hspmv_exchange(self._h, C.byref(b), C.byref(g)), "hspmv_exchange")
+        return b.value, g.value
+
+    @property
+    def info(self) -> dict:
+        i = _lib.Info()
+        check(lib().hspmv_get_info(self._h, C.byref(i)), "hspmv_get_info")
+        d = {k: getattr(i, k) for k, _ in _lib.Info._fields_}
+        d["kernel_name"] = KERNEL_NAMES.get(d["kernel"], "?")
+        return d
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().hspmv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

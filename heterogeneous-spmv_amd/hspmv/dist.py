@@ -1,0 +1,131 @@
+"""Row-range partition across ranks (one process per GPU), SURVEY.md §8e.
+
+The reference has no multi-device code (only a cudaGetDeviceCount print,
+cuda-spmv-csrk/cuda/spmv-auto-ampere.cu:200-203); this is new.  Rows are
+independent, so the SpMV itself shards with no collective: rank r owns a
+contiguous, nnz-balanced row range [splits[r], splits[r+1]) with global column
+indices, and needs the whole x.  The two exchange steps of the path are
+
+  * x broadcast from rank 0 (``broadcast_x``), once per new x;
+  * y gather into a full-length vector (``gather_y``): an all-gather of the
+    shards padded to the longest one, then unpadded.
+
+Both go through ``torch.distributed`` (backend "nccl" = RCCL over xGMI on the
+GPU box, "gloo" on the CPU in tests).  Workloads are built per rank from the
+seeded generators in :mod:`hspmv.gen`, so no rank ever materialises the global
+matrix.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import gen
+from .api import CsrMatrix, partition_rows
+
+
+# ------------------------------------------------------------------ workloads
+
+@dataclass
+class Shard:
+    A: CsrMatrix          # this rank's rows (row_ptr rebased, global columns)
+    n_global: int         # length of x
+    m_global: int
+    nnz_global: int
+    splits: np.ndarray    # row ranges of all ranks (world+1)
+    rank: int
+    world: int
+    name: str
+    scaling: str          # "weak" (per-rank work fixed) or "strong"
+
+
+def laplace2d_row_nnz(nx: int, ny: int) -> np.ndarray:
+    """Row lengths of the 5-point Laplacian on nx x ny (no columns built)."""
+    m = nx * ny
+    r = np.arange(m, dtype=np.int64)
+    ix = r % nx
+    return (1 + (r >= nx) + (ix > 0) + (ix < nx - 1) + (r < m - nx)).astype(np.int64)
+
+
+def banded_row_nnz(m: int, per_row: int = 10, half: int = 32, seed: int = 11) -> np.ndarray:
+    """Row lengths of gen.banded (only the first/last `half` rows lose columns)."""
+    cnt = np.full(m, per_row, np.int64)
+    edge = min(half, m)
+    for r0, r1 in ((0, edge), (max(m - edge, 0), m)):
+        if r1 > r0:
+            cnt[r0:r1] = np.diff(gen.banded(m, per_row, half, seed, r0=r0, r1=r1).row_ptr)
+    return cnt
+
+
+def splits_from_row_nnz(row_nnz: np.ndarray, world: int) -> np.ndarray:
+    rp = np.zeros(row_nnz.shape[0] + 1, np.int64)
+    np.cumsum(row_nnz, out=rp[1:])
+    if rp[-1] >= 2 ** 31:
+        # int32 row_ptr cannot hold it: balance on the int64 prefix sum directly
+        targets = rp[-1] * np.arange(world + 1) // world
+        s = np.searchsorted(rp, targets, side="left").astype(np.int64)
+        s[0], s[-1] = 0, row_nnz.shape[0]
+        return s
+    return partition_rows(rp.astype(np.int32), world)
+
+
+def build_shard(config: str, rank: int, world: int, dtype=np.float64) -> Shard:
+    """c2: 5-pt Laplacian, 1000 x 1000 rows per rank (global grid 1000 x 1000*world,
+           weak scaling; world = 1 is BASELINE configs[1] exactly).
+       c4: banded m = 2e7 (BASELINE configs[3]) split over the ranks (strong).
+       small: 5-pt Laplacian 64 x 64 per rank (tests)."""
+    if config in ("c2", "small"):
+        nx = 1000 if config == "c2" else 64
+        ny = nx * world
+        row_nnz = laplace2d_row_nnz(nx, ny)
+        splits = splits_from_row_nnz(row_nnz, world)
+        A = gen.laplace2d(nx, ny, int(splits[rank]), int(splits[rank + 1]), dtype=dtype)
+        return Shard(A, nx * ny, nx * ny, int(row_nnz.sum()), splits, rank, world,
+                     f"5-pt Laplacian {nx}x{ny} (fp64 CSR), {nx}x{nx} rows per GPU", "weak")
+    if config == "c4":
+        m = 20_000_000
+        row_nnz = banded_row_nnz(m)
+        splits = splits_from_row_nnz(row_nnz, world)
+        A = gen.banded(m, r0=int(splits[rank]), r1=int(splits[rank + 1]), dtype=dtype)
+        return Shard(A, m, m, int(row_nnz.sum()), splits, rank, world,
+                     "banded m=2e7, 10 nnz/row within +-32 (fp64 CSR)", "strong")
+    raise ValueError(f"unknown distributed config {config!r}")
+
+
+# ------------------------------------------------------------------ exchanges
+
+def broadcast_x(x, src: int = 0) -> None:
+    """In-place broadcast of the full x (a torch tensor) from rank src."""
+    import torch.distributed as dist
+    dist.broadcast(x, src)
+
+
+def gather_y(y_local, splits: np.ndarray):
+    """All-gather the row shards into a full-length y on every rank (padded
+    all-gather, then unpadded).  y_local: torch tensor of this rank's rows."""
+    import torch
+    import torch.distributed as dist
+    world = len(splits) - 1
+    rows = np.diff(splits)
+    pad = int(rows.max())
+    buf = torch.zeros(pad, dtype=y_local.dtype, device=y_local.device)
+    buf[: y_local.shape[0]] = y_local
+    out = torch.empty(pad * world, dtype=y_local.dtype, device=y_local.device)
+    dist.all_gather_into_tensor(out, buf)
+    parts = [out[r * pad: r * pad + int(rows[r])] for r in range(world)]
+    return torch.cat(parts)
+
+
+def checksum_ok(A: CsrMatrix, x: np.ndarray, y: np.ndarray, seed: int = 99) -> tuple[bool, float]:
+    """Size-independent identity w.(A x) == (A^T w).x in fp64 -- a property
+    check of the GPU y that needs neither the oracle nor a second SpMV path."""
+    w = gen.rand_x(A.m, seed)
+    lhs = float(np.dot(w, y.astype(np.float64)))
+    rows = np.repeat(np.arange(A.m), np.diff(A.row_ptr))
+    atw = np.bincount(A.col_idx, weights=A.val.astype(np.float64) * w[rows], minlength=A.n)
+    rhs = float(np.dot(atw, x.astype(np.float64)))
+    scale = float(np.dot(np.abs(w)[rows], np.abs(A.val.astype(np.float64) * x[A.col_idx]))) + 1e-300
+    rel = abs(lhs - rhs) / scale
+    tol = 1e-12 if A.val.dtype == np.float64 else 1e-5
+    return rel <= tol, rel

@@ -1,0 +1,230 @@
+/*
+ * hspmv.h -- C ABI of the MI355X-native CSR / CSR-3 SpMV library
+ * (libhspmv.so, built from heterogeneous-spmv_amd/csrc/).
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference
+ * has no library: its "boundary" is three things, each replaced here
+ * (SURVEY.md §8b):
+ *
+ *  1. Kernel ABI  -- cuda_spmv (cuda-spmv-csr/spmv.cu:117-119) and
+ *     cuSpMV_3 / cuSpMV_3_vec / cuSpMV_2 (cuda-spmv-csrk/hip/csrk.cuh:25-47),
+ *     all taking raw device pointers.  Replaced by hspmv_spmv() on a handle
+ *     that owns (or borrows, HSPMV_FLAG_DEVICE_PTRS) the device arrays.
+ *  2. Host library -- CSRk_Graph(nRows, nCols, nnz, rVec, cVec, val, ...,
+ *     k, supRowSizes) + putInCSRkFormat() / setX() / setY() / getY()
+ *     (cuda-spmv-csrk/hip/csrk.cuh:321-353, csrk.cu:92-113, 531-641, 875-900).
+ *     Replaced by hspmv_create() (+ hspmv_build_csr3_maps()), hspmv_set_x(),
+ *     hspmv_get_y().
+ *  3. CLI/stdout contract -- spmv-csr/spmv.c:116-225 and
+ *     cuda-spmv-csrk/hip/spmv*.cu; reproduced by the spmv-csr / spmv-csrk
+ *     executables built on top of this header.
+ *
+ * Conventions: every int-returning function returns 0 on success and a
+ * negative HSPMV_E* code on failure (the reference ignores every hip* status;
+ * SURVEY.md §5).  hspmv_last_error() returns a thread-local message.  No C++
+ * exceptions cross this boundary.  Indices are 0-based int32 (readers accept
+ * 1-based files and rebase them).  Values are fp32 or fp64 (hspmv_dtype).
+ */
+#ifndef HSPMV_H
+#define HSPMV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HSPMV_VERSION_MAJOR 0
+#define HSPMV_VERSION_MINOR 1
+
+/* ---------------------------------------------------------------- status */
+#define HSPMV_OK 0
+#define HSPMV_E_INVALID (-1)   /* bad argument / malformed matrix          */
+#define HSPMV_E_IO (-2)        /* file cannot be opened / parsed           */
+#define HSPMV_E_NOMEM (-3)     /* host or device allocation failed         */
+#define HSPMV_E_HIP (-4)       /* HIP runtime error                        */
+#define HSPMV_E_RCCL (-5)      /* RCCL error                               */
+#define HSPMV_E_NODEV (-6)     /* no / not enough HIP devices              */
+#define HSPMV_E_STATE (-7)     /* call order violated (e.g. run before x)  */
+
+/* ---------------------------------------------------------------- types */
+typedef enum { HSPMV_F32 = 0, HSPMV_F64 = 1 } hspmv_dtype;
+
+/* A CSR matrix.  Borrowed: the library copies (or, with
+ * HSPMV_FLAG_DEVICE_PTRS, references) the arrays during hspmv_create only. */
+typedef struct {
+  int64_t m, n, nnz;
+  const int32_t *row_ptr; /* m+1 entries, row_ptr[0] == 0                */
+  const int32_t *col_idx; /* nnz entries, 0 <= col < n                   */
+  const void *val;        /* nnz entries of dtype                        */
+  int32_t dtype;          /* hspmv_dtype                                 */
+} hspmv_csr;
+
+/* CSR-3 multilevel maps (A12/A13 in SURVEY.md §8a):
+ * super-super-row s covers super-rows outer[s] .. outer[s+1]-1,
+ * super-row r covers rows inner[r] .. inner[r+1]-1.
+ * Same meaning as mapCoarseToFinerRows[2] / [1] of the reference
+ * (csrk.cu:1614, .csr3 writer spmv-auto.cpp:38-62). */
+typedef struct {
+  int64_t n_ssr, n_sr;
+  const int32_t *outer; /* n_ssr+1 */
+  const int32_t *inner; /* n_sr+1  */
+} hspmv_csr3_maps;
+
+/* Owned buffers returned by the readers / builders; free with the matching
+ * hspmv_free_* call. */
+typedef struct {
+  int64_t m, n, nnz;
+  int32_t *row_ptr;
+  int32_t *col_idx;
+  void *val;
+  int32_t dtype;
+  int32_t index_base; /* base found in the file (0 or 1); arrays are 0-based */
+} hspmv_csr_buf;
+
+typedef struct {
+  int64_t n_ssr, n_sr;
+  int32_t *outer;
+  int32_t *inner;
+} hspmv_csr3_buf;
+
+/* Timing of hspmv_run: the reference protocol (5 warm-ups, N timed runs,
+ * min/max/avg; spmv-csr/spmv.c:164-185, hip/spmv-auto-mi100.cu:200-240).
+ * t_* are device times from HIP events around each SpMV (max over GPUs);
+ * wall_* are host steady_clock times around launch + synchronize, which is
+ * what the reference measures. */
+typedef struct {
+  double t_min, t_max, t_avg;
+  double wall_min, wall_max, wall_avg;
+  double gflops;   /* 2*nnz / t_min * 1e-9                                 */
+  double gbps_alg; /* hspmv_alg_bytes() / t_min * 1e-9                     */
+  int32_t iters;
+  int32_t num_gpus;
+} hspmv_timing;
+
+/* What a handle decided (kernel, launch shape, bytes). */
+typedef struct {
+  int32_t kernel;     /* HSPMV_KERNEL_* actually used                      */
+  int32_t lanes;      /* lanes per row (VECTOR) / rows per wave task       */
+  int32_t waves_per_block;
+  int32_t num_gpus;
+  int64_t blocks;     /* grid size of the launch (GPU 0)                   */
+  double alg_bytes;   /* algorithmic bytes per SpMV        */
+  double flops;       /* 2 * nnz                                           */
+  int64_t device_bytes; /* device memory held by the handle (all GPUs)     */
+} hspmv_info;
+
+typedef struct hspmv_handle hspmv_handle;
+
+/* ---------------------------------------------------------------- flags */
+#define HSPMV_KERNEL_AUTO 0u   /* STREAM for CSR, CSR3 when maps given    */
+#define HSPMV_KERNEL_VECTOR 1u /* L lanes (sub-wave) per row, shuffle sum  */
+#define HSPMV_KERNEL_STREAM 2u /* wave per 64-row group, LDS-staged,
+                                  ordered per-row sums (bit-exact vs CPU)  */
+#define HSPMV_KERNEL_CSR3 3u   /* workgroup per super-super-row, waves
+                                  balanced over super-rows by nnz         */
+#define HSPMV_KERNEL_MASK 0xFu
+/* lanes per row for VECTOR: HSPMV_LANES(L), L in {1,2,4,8,16,32,64}; 0=auto */
+#define HSPMV_LANES_SHIFT 4
+#define HSPMV_LANES(l) ((unsigned)(l) << HSPMV_LANES_SHIFT)
+#define HSPMV_LANES_MASK (0x7Fu << HSPMV_LANES_SHIFT)
+#define HSPMV_FLAG_NONTEMPORAL (1u << 12) /* nt loads for val/col streams  */
+#define HSPMV_FLAG_DEVICE_PTRS (1u << 13) /* A/maps are device pointers on
+                                             the target device (borrowed)  */
+
+/* ---------------------------------------------------------------- handle */
+/* Upload A (and optional CSR-3 maps) to num_gpus devices (0 = all visible).
+ * With num_gpus > 1 the rows are partitioned into nnz-balanced contiguous
+ * ranges (on super-super-row boundaries when maps are given), x is
+ * broadcast and y gathered with RCCL.  Replaces the CSRk_Graph constructor +
+ * the H2D uploads of csrk.cu:580-587 / 847-865 and cuda-spmv-csr/spmv.cu:66-71. */
+int hspmv_create(hspmv_handle **h, const hspmv_csr *A,
+                 const hspmv_csr3_maps *maps, int num_gpus, unsigned flags);
+
+/* Single-device handle on `device`, launching on `stream` (a hipStream_t;
+ * NULL = the library creates one).  This is the entry a one-process-per-GPU
+ * caller (torch.distributed, MPI) uses for its row-range shard. */
+int hspmv_create_on_device(hspmv_handle **h, const hspmv_csr *A,
+                           const hspmv_csr3_maps *maps, int device,
+                           void *stream, unsigned flags);
+
+/* x (n entries of dtype) from host memory -> every GPU (setX, csrk.cu:92-102,
+ * minus the x permutation: matrices are used as given). */
+int hspmv_set_x(hspmv_handle *h, const void *x_host);
+/* Bind caller-owned device vectors (single-device handles).  x: n entries,
+ * y: m entries, on the handle's device.  NULL restores the handle's own. */
+int hspmv_bind_x_device(hspmv_handle *h, const void *x_dev);
+int hspmv_bind_y_device(hspmv_handle *h, void *y_dev);
+/* Device pointers currently used for x / y on GPU `gpu`. */
+void *hspmv_x_device(hspmv_handle *h, int gpu);
+void *hspmv_y_device(hspmv_handle *h, int gpu);
+
+/* Enqueue ONE y = A*x on the handle's stream(s).  Asynchronous; the hot path. */
+int hspmv_spmv(hspmv_handle *h);
+int hspmv_synchronize(hspmv_handle *h);
+
+/* Reference timing protocol: warmup SpMVs, then iters timed SpMVs, each
+ * bracketed by events + synchronize (hip/spmv-auto-mi100.cu:214-236). */
+int hspmv_run(hspmv_handle *h, int warmup, int iters, hspmv_timing *out);
+
+/* y (m entries of dtype) -> host; gathers the shards of a multi-GPU handle
+ * (getY, csrk.cu:110-113). */
+int hspmv_get_y(hspmv_handle *h, void *y_host);
+
+/* Multi-GPU only: RCCL broadcast of x from GPU 0 and all-gather of y into
+ * every GPU's full-length buffer, timed (seconds).  Either pointer may be NULL. */
+int hspmv_exchange(hspmv_handle *h, double *bcast_x_s, double *gather_y_s);
+
+int hspmv_get_info(hspmv_handle *h, hspmv_info *out);
+void hspmv_destroy(hspmv_handle *h);
+
+/* ---------------------------------------------------------------- formats */
+/* Text .csr reader (spmv-csr/spmv.c:11-57 layout; index base auto-detected
+ * from row_ptr[0]; values parsed correctly rounded into dtype). */
+int hspmv_read_csr(const char *path, int dtype, hspmv_csr_buf *out);
+/* Text .csr3 reader (reformat-csr-to-csr3/stats.c:10-79 layout). */
+int hspmv_read_csr3(const char *path, int dtype, hspmv_csr_buf *A,
+                    hspmv_csr3_buf *maps);
+/* Writers (reference text layouts: helpers/sparse2csr.m:1-7 for .csr,
+ * reformat-csr-to-csr3/spmv-auto.cpp:30-65 for .csr3; values "%.6f"). */
+int hspmv_write_csr(const char *path, const hspmv_csr *A);
+int hspmv_write_csr3(const char *path, const hspmv_csr *A,
+                     const hspmv_csr3_maps *maps);
+/* Binary cache: raw little-endian arrays. */
+int hspmv_save_bin(const char *path, const hspmv_csr *A,
+                   const hspmv_csr3_maps *maps);
+int hspmv_load_bin(const char *path, hspmv_csr_buf *A, hspmv_csr3_buf *maps);
+void hspmv_free_csr(hspmv_csr_buf *A);
+void hspmv_free_csr3(hspmv_csr3_buf *maps);
+
+/* ---------------------------------------------------------------- CSR-3 */
+/* Build CSR-3 maps in file order with the handCoarsen grouping rule
+ * (csrk.cu:1438-1484) and level thresholds supRowSizes[i-1]*NNZ/N
+ * (csrk.cu:1089-1091).  ssrs = rows->super-rows size, srs =
+ * super-rows->super-super-rows size. */
+int hspmv_build_csr3_maps(const hspmv_csr *A, int ssrs, int srs,
+                          hspmv_csr3_buf *out);
+/* Auto parameters.  flavour 0: the .csr3 writer / Volta formula
+ * (reformat-csr-to-csr3/spmv-auto.cpp:154-173); 1: the MI100 driver formula
+ * (hip/spmv-auto-mi100.cu:130-158); 2: this library's MI355X choice. */
+int hspmv_csr3_params(double nnz_per_row, int flavour, int *ssrs, int *srs);
+
+/* ---------------------------------------------------------------- misc */
+/* nnz-balanced contiguous row ranges: splits[0]=0 .. splits[parts]=m, with
+ * row_ptr[splits[p]] ~ p*nnz/parts.  With maps != NULL splits fall on
+ * super-super-row boundaries. */
+int hspmv_partition_rows(int64_t m, const int32_t *row_ptr,
+                         const hspmv_csr3_maps *maps, int parts,
+                         int64_t *splits);
+/* Algorithmic bytes of one SpMV:
+ * nnz*(sv+4) + (m+1)*4 + n*sv + m*sv (+ (n_ssr+1 + n_sr+1)*4 for CSR-3). */
+double hspmv_alg_bytes(int64_t m, int64_t n, int64_t nnz, int dtype,
+                       int64_t n_ssr, int64_t n_sr);
+int hspmv_device_count(int *count);
+const char *hspmv_last_error(void);
+const char *hspmv_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HSPMV_H */

@@ -1,0 +1,234 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+Bar (BASELINE.json north star): fp64 y within
+    |y - y64| <= 1e-6 |y64| + 1e-12 * sum_k |a_k x_k|
+of the spmv-csr restatement.  The STREAM / CSR3 kernels sum each row in the
+reference order with the reference rounding, so on rows up to 32 nonzeros
+they are checked BITWISE: fp32 against the reference binary's own golden
+output, fp64 against the restatement.
+"""
+import numpy as np
+import pytest
+
+import hspmv
+import oracle
+from conftest import GOLDEN, fp64_tol_ok, load_golden
+from hspmv import gen
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = [("stream", 0), ("vector", 1), ("vector", 2), ("vector", 4), ("vector", 8),
+           ("vector", 16), ("vector", 32), ("vector", 64), ("auto", 0)]
+SERIAL_MAX = 32  # rows up to this length go through the ordered (bit-exact) path
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    n = hspmv.device_count()
+    assert n >= 1, "no HIP device visible: the gpu tests must run on the MI355X box"
+
+
+def gpu_spmv(A, x, maps=None, **kw):
+    with hspmv.SpMV(A, maps, **kw) as op:
+        return op(x), op.info
+
+
+def check_fp64(A, x, y, exact_rows=None):
+    y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    assert fp64_tol_ok(y, y64, absrow), np.abs(y - y64).max()
+    if exact_rows is not None:
+        assert np.array_equal(y[exact_rows], y64[exact_rows])
+    return y64
+
+
+def short_rows(A):
+    return np.diff(A.row_ptr) <= SERIAL_MAX
+
+
+def test_golden_fp32_bitwise_vs_reference_binary(golden_names):
+    """STREAM / CSR3 in fp32 reproduce the reference's own omp_spmv output
+    bit for bit on every row of up to 32 nonzeros (x = 1 and x = rand)."""
+    for name in golden_names:
+        A = hspmv.read_csr(GOLDEN / f"{name}.csr", np.float32)
+        g = load_golden(name)
+        ok = short_rows(A)
+        x = gen.rand_x(A.n, 42).astype(np.float32)
+        for kernel in ("stream", "auto"):
+            y, _ = gpu_spmv(A, x, kernel=kernel)
+            assert np.array_equal(y[ok].view(np.uint32), g["y_ref_f32_rand"][ok].view(np.uint32)), name
+            if "y_ref_f32_ones" in g:
+                y1, _ = gpu_spmv(A, np.ones(A.n, np.float32), kernel=kernel)
+                assert np.array_equal(y1[ok].view(np.uint32), g["y_ref_f32_ones"][ok].view(np.uint32))
+            # long rows: within fp32 accumulation error of the reference
+            if (~ok).any():
+                absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+                nrow = np.diff(A.row_ptr)
+                err = np.abs(y.astype(np.float64) - g["y_ref_f32_rand"])
+                assert np.all(err <= (nrow + 2) * 2.0 ** -23 * absrow + 1e-30)
+
+
+def test_golden_fp64_all_kernels(golden_names):
+    for name in golden_names:
+        A = hspmv.read_csr(GOLDEN / f"{name}.csr", np.float64)
+        g = load_golden(name)
+        x = gen.rand_x(A.n, 42)
+        absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+        for kernel, lanes in KERNELS:
+            y, info = gpu_spmv(A, x, kernel=kernel, lanes=lanes)
+            assert fp64_tol_ok(y, g["y_orc_f64_rand"], absrow), (name, kernel, lanes)
+            if kernel in ("stream", "auto"):
+                ok = short_rows(A)
+                assert np.array_equal(y[ok], g["y_orc_f64_rand"][ok]), (name, kernel)
+
+
+def test_golden_csr3_fixtures(manifest):
+    for name, ent in manifest["fixtures"].items():
+        if "csr3" not in ent:
+            continue
+        for dt in (np.float64, np.float32):
+            A, maps = hspmv.read_csr3(GOLDEN / f"{name}.csr3", dt)
+            x = gen.rand_x(A.n, 42).astype(dt)
+            y, info = gpu_spmv(A, x, maps, kernel="csr3")
+            assert info["kernel_name"] == "csr3"
+            ok = short_rows(A)
+            y_ref = oracle.csr3_spmv(maps.outer, maps.inner, A.row_ptr, A.col_idx, A.val, x)
+            assert np.array_equal(y[ok], y_ref[ok]), (name, dt)
+            if dt == np.float64:
+                check_fp64(A, x, y)
+
+
+@pytest.mark.parametrize("waves_case", [(7, 8), (20, 10), (64, 4), (1, 1), (400, 2)])
+def test_csr3_map_sizes(waves_case):
+    """Any map granularity (tiny super-rows, one-row super-rows, huge SSRs
+    that need several waves and several 64-row groups) gives the same y."""
+    ssrs, srs = waves_case
+    for A in (gen.laplace2d(300, 200), gen.powerlaw(30000, seed=11, dtype=np.float64)):
+        maps = hspmv.build_csr3_maps(A, ssrs, srs)
+        x = gen.rand_x(A.n, 5)
+        y, info = gpu_spmv(A, x, maps)
+        assert info["kernel_name"] == "csr3"
+        check_fp64(A, x, y, exact_rows=short_rows(A))
+
+
+def test_nontemporal_variants_identical():
+    A = gen.stencil27(20)
+    x = gen.rand_x(A.n, 8)
+    for kernel in ("stream", "vector"):
+        y0, _ = gpu_spmv(A, x, kernel=kernel)
+        y1, _ = gpu_spmv(A, x, kernel=kernel, nontemporal=True)
+        assert np.array_equal(y0, y1)
+    maps = hspmv.build_csr3_maps(A, 20, 10)
+    y0, _ = gpu_spmv(A, x, maps)
+    y1, _ = gpu_spmv(A, x, maps, nontemporal=True)
+    assert np.array_equal(y0, y1)
+
+
+def test_edge_cases():
+    # empty matrix rows, all-empty matrix, single row, single column, zero nnz
+    cases = []
+    cases.append(hspmv.CsrMatrix(5, 7, np.zeros(6, np.int32), np.zeros(0, np.int32),
+                                 np.zeros(0, np.float64)))
+    cases.append(hspmv.CsrMatrix(1, 1, np.array([0, 1]), np.array([0]), np.array([2.5])))
+    cases.append(hspmv.CsrMatrix(3, 1, np.array([0, 1, 1, 2]), np.array([0, 0]),
+                                 np.array([1.0, -3.0])))
+    rng = np.random.default_rng(1)
+    for m in (63, 64, 65, 127, 129, 1000):  # around the 64-row wave tasks
+        lens = rng.integers(0, 80, m)
+        rp = np.concatenate([[0], np.cumsum(lens)])
+        ci = rng.integers(0, 500, rp[-1])
+        cases.append(hspmv.CsrMatrix(m, 500, rp, ci, rng.uniform(-1, 1, rp[-1])))
+    for A in cases:
+        x = gen.rand_x(A.n, 1)
+        for kernel, lanes in KERNELS:
+            y, _ = gpu_spmv(A, x, kernel=kernel, lanes=lanes)
+            check_fp64(A, x, y)
+        if A.m > 1:
+            maps = hspmv.build_csr3_maps(A, 3, 2)
+            y, _ = gpu_spmv(A, x, maps)
+            check_fp64(A, x, y, exact_rows=short_rows(A))
+
+
+def test_repeated_spmv_and_rebinding():
+    A = gen.banded(100000, seed=3)
+    x1, x2 = gen.rand_x(A.n, 1), gen.rand_x(A.n, 2)
+    with hspmv.SpMV(A) as op:
+        y1 = op(x1)
+        y2 = op(x2)
+        for _ in range(10):
+            op.spmv()
+        op.synchronize()
+        assert np.array_equal(op.get_y(), y2)
+        t = op.run(warmup=2, iters=5)
+        assert t["iters"] == 5 and t["t_min"] > 0 and t["gflops"] > 0
+    check_fp64(A, x1, y1)
+    # linearity: A(2 x1 - x2) = 2 A x1 - A x2 (fp64 rounding only)
+    with hspmv.SpMV(A) as op:
+        y3 = op(2 * x1 - x2)
+    np.testing.assert_allclose(y3, 2 * y1 - y2, atol=1e-12 * np.abs(A.val).max() * 20)
+
+
+def test_errors_are_reported_not_crashes():
+    A = gen.laplace2d(10, 10)
+    with hspmv.SpMV(A) as op:
+        with pytest.raises(hspmv.HspmvError, match="E_STATE"):
+            op.spmv()  # x not set
+        with pytest.raises(ValueError):
+            op.set_x(np.zeros(3))
+    bad = hspmv.CsrMatrix(2, 2, np.array([0, 1, 2]), np.array([0, 9]), np.array([1.0, 1.0]))
+    with pytest.raises(hspmv.HspmvError, match="E_INVALID"):
+        hspmv.SpMV(bad)
+    with pytest.raises(hspmv.HspmvError, match="E_NODEV"):
+        hspmv.SpMV(A, device=999)
+    with pytest.raises(hspmv.HspmvError):
+        hspmv.SpMV(A, num_gpus=hspmv.device_count() + 1)
+
+
+# ---------------------------------------------------------------- full size
+
+def test_config_c2_laplacian_1m_fp64():
+    """BASELINE configs[1]: CSR fp64 on the 1000x1000 Laplacian, x = 1 and rand."""
+    A = gen.laplace2d(1000, 1000)
+    assert A.nnz == 4_996_000
+    for x in (np.ones(A.n), gen.rand_x(A.n, 42)):
+        for kernel in ("auto", "vector"):
+            y, info = gpu_spmv(A, x, kernel=kernel)
+            check_fp64(A, x, y, exact_rows=slice(None) if kernel == "auto" else None)
+
+
+def test_config_c3_stencil27_csr3_fp64():
+    """BASELINE configs[2] stand-in: 27-pt 125^3 RCM, CSR-3 with ssrs=20, srs=10."""
+    A = gen.stencil27(125)
+    assert A.nnz == 51_895_117
+    ssrs, srs = hspmv.csr3_params(A.nnz / A.m, "volta")
+    assert (ssrs, srs) == (20, 10)
+    maps = hspmv.build_csr3_maps(A, ssrs, srs)
+    x = gen.rand_x(A.n, 7)
+    y, info = gpu_spmv(A, x, maps)
+    check_fp64(A, x, y, exact_rows=slice(None))
+
+
+def test_config_c4_banded_shard_fp64():
+    """BASELINE configs[3]: one rank's row-range shard of the 2e7-row banded
+    matrix (P = 8 -> 2.5 M rows), global columns, full-length x."""
+    m = 20_000_000
+    splits = np.linspace(0, m, 9).astype(np.int64)
+    A = gen.banded(m, r0=int(splits[3]), r1=int(splits[4]))
+    x = gen.rand_x(m, 11)
+    y, _ = gpu_spmv(A, x)
+    check_fp64(A, x, y, exact_rows=slice(None))
+
+
+def test_config_c5_powerlaw_csr3_fp32():
+    """BASELINE configs[4]: power-law fp32, CSR-3, long rows on the wave path."""
+    A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32)
+    maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
+    x = gen.rand_x(A.n, 9).astype(np.float32)
+    y, info = gpu_spmv(A, x, maps)
+    y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    ok = short_rows(A)
+    assert np.array_equal(y[ok].view(np.uint32), y32[ok].view(np.uint32))
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    nrow = np.diff(A.row_ptr)
+    err = np.abs(y.astype(np.float64) - y32.astype(np.float64))
+    assert np.all(err <= (nrow + 2) * 2.0 ** -23 * absrow + 1e-30)

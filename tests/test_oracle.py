@@ -1,0 +1,109 @@
+"""The oracle (CPU restatement) pinned against the reference's own outputs.
+
+The golden y vectors were produced by the reference's spmv-csr/spmv.c compiled
+unmodified (tests/golden/make_golden.py); the restatement must reproduce them
+bit for bit in fp32.  When the reference build is present (this container),
+the restatement is also re-checked against it live on fresh inputs.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN, load_golden
+from hspmv import gen
+
+
+def test_oracle_matches_reference_golden_fp32_bitwise(golden_names):
+    for name in golden_names:
+        m, n, rp, ci, v32, v64, base = oracle.read_csr(GOLDEN / f"{name}.csr")
+        g = load_golden(name)
+        x32 = gen.rand_x(n, 42).astype(np.float32)
+        y = oracle.spmv(rp, ci, v32, x32)
+        assert np.array_equal(y.view(np.uint32), g["y_ref_f32_rand"].view(np.uint32)), name
+        if "y_ref_f32_ones" in g:
+            y1 = oracle.spmv(rp, ci, v32, np.ones(n, np.float32))
+            assert np.array_equal(y1.view(np.uint32), g["y_ref_f32_ones"].view(np.uint32)), name
+
+
+def test_oracle_fp64_golden_and_serial_equals_parallel(golden_names):
+    for name in golden_names:
+        m, n, rp, ci, v32, v64, base = oracle.read_csr(GOLDEN / f"{name}.csr")
+        x = gen.rand_x(n, 42)
+        y = oracle.spmv(rp, ci, v64, x)
+        ys = oracle.spmv(rp, ci, v64, x, serial=True)
+        assert np.array_equal(y, ys)
+        assert np.array_equal(y, load_golden(name)["y_orc_f64_rand"]), name
+
+
+def test_oracle_fp64_close_to_fp32_reference(golden_names):
+    # the fp64 restatement agrees with the fp32 reference at fp32 accuracy
+    for name in golden_names:
+        m, n, rp, ci, v32, v64, base = oracle.read_csr(GOLDEN / f"{name}.csr")
+        x = gen.rand_x(n, 42)
+        g = load_golden(name)
+        absrow = oracle.abs_rowsum(rp, ci, v64, x)
+        nrow = np.diff(rp).astype(np.float64)
+        err = np.abs(g["y_ref_f32_rand"].astype(np.float64) - g["y_orc_f64_rand"])
+        assert np.all(err <= (nrow + 2) * 2.0 ** -23 * absrow + 1e-6), name
+
+
+def test_oracle_matches_scipy():
+    A = gen.laplace2d(50, 40)
+    x = gen.rand_x(A.n, 3)
+    y = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    np.testing.assert_allclose(y, A.to_scipy() @ x, rtol=1e-14, atol=1e-14)
+
+
+def test_one_based_file_reads_identically():
+    a = oracle.read_csr(GOLDEN / "lap32.mtx.rcm.csr")
+    b = oracle.read_csr(GOLDEN / "lap32.onebased.csr")
+    assert b[6] == 1 and a[6] == 0
+    for u, v in zip(a[:6], b[:6]):
+        assert np.array_equal(u, v)
+
+
+def test_csr3_fixture_maps_and_spmv(manifest):
+    for name, ent in manifest["fixtures"].items():
+        if "csr3" not in ent:
+            continue
+        outer, inner, m, n, rp, ci, v32, v64 = oracle.read_csr3(GOLDEN / f"{name}.csr3")
+        maps = np.load(GOLDEN / f"{name}.maps.npz")
+        assert np.array_equal(outer, maps["outer"]) and np.array_equal(inner, maps["inner"])
+        # A13 invariants: maps monotone and complete
+        assert outer[0] == 0 and outer[-1] == len(inner) - 1
+        assert inner[0] == 0 and inner[-1] == m
+        assert np.all(np.diff(outer) >= 0) and np.all(np.diff(inner) >= 0)
+        x = gen.rand_x(n, 42)
+        y3 = oracle.csr3_spmv(outer, inner, rp, ci, v64, x)
+        assert np.array_equal(y3, load_golden(name)["y_orc_f64_rand"])
+        # rebuilding the maps reproduces the fixture
+        o2, i2 = oracle.build_maps(rp, ci, ent["csr3"]["ssrs"], ent["csr3"]["srs"])
+        assert np.array_equal(o2, outer) and np.array_equal(i2, inner)
+
+
+def test_hand_coarsen_grouping_rule():
+    # every super-row but the last holds >= threshold nnz and drops below it
+    # without its last row (csrk.cu:1450-1484)
+    A = gen.powerlaw(3000, seed=5, dtype=np.float64)
+    ssrs, srs = 7, 8
+    outer, inner = oracle.build_maps(A.row_ptr, A.col_idx, ssrs, srs)
+    thr = ssrs * A.nnz // A.m
+    for s in range(len(inner) - 2):
+        a, b = inner[s], inner[s + 1]
+        assert A.row_ptr[b] - A.row_ptr[a] >= thr
+        assert A.row_ptr[b - 1] - A.row_ptr[a] < thr
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="reference build not present (GPU box)")
+def test_oracle_matches_live_reference_fp32(tmp_path):
+    for seed, A in enumerate([gen.powerlaw(4000, seed=9, dtype=np.float64),
+                              gen.banded(5000, seed=3), gen.laplace2d(40, 60)]):
+        p = tmp_path / f"m{seed}.csr"
+        gen.write_csr_text(str(p), A)
+        m, n, rp, ci, v32, v64, base = oracle.read_csr(p)
+        x = gen.rand_x(n, 100 + seed).astype(np.float32)
+        y_ref = oracle.ref_spmv_file(p, x)
+        y_ser = oracle.ref_spmv_file(p, x, serial=True)
+        y = oracle.spmv(rp, ci, v32, x)
+        assert np.array_equal(y.view(np.uint32), y_ref.view(np.uint32))
+        assert np.array_equal(y_ser.view(np.uint32), y_ref.view(np.uint32))
