@@ -1,0 +1,108 @@
+"""The spmv-csr / spmv-csrk executables keep the reference's command line and
+stdout contract (TimeMin/TimeMax/TimeAvg in seconds, Number Wrong), parsed the
+way run_scripts/run_norm.py:94-107 parses it."""
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN, REPO
+from hspmv import gen
+
+BUILD = REPO / "heterogeneous-spmv_amd" / "build"
+
+
+def run(*args, check=True):
+    p = subprocess.run([str(a) for a in args], capture_output=True, text=True, timeout=300)
+    if check and p.returncode != 0:
+        raise AssertionError(f"{args} -> {p.returncode}\n{p.stdout}\n{p.stderr}")
+    return p
+
+
+def harness_parse(out: str):
+    # run_norm.py:94-107: find("TimeMin:") + 8 chars to end of line
+    vals = []
+    for key in ("TimeMin:", "TimeMax:", "TimeAvg:"):
+        i = out.find(key)
+        j = out.find("\n", i)
+        vals.append(float(out[i + 8:j]))
+    return vals
+
+
+def test_usage_without_gpu():
+    # argc < 3 prints the usage line and exits 0 (spmv-csr/spmv.c:118-121)
+    p = run(BUILD / "spmv-csr")
+    assert "num_runs" in p.stdout
+    p = run(BUILD / "spmv-csrk")
+    assert "num_runs" in p.stdout
+
+
+@pytest.mark.gpu
+def test_spmv_csr_contract_and_check(tmp_path):
+    for name in ("lap32.mtx.rcm", "powerlaw1500", "long_row", "empty_rows"):
+        for dtype in ("f64", "f32"):
+            p = run(BUILD / "spmv-csr", GOLDEN / f"{name}.csr", 7, "--dtype", dtype, "--x", "rand:42")
+            tmin, tmax, tavg = harness_parse(p.stdout)
+            assert 0 < tmin <= tavg <= tmax
+            assert "Number Wrong: 0" in p.stdout
+            assert "Check: PASS" in p.stdout
+            assert "TEAST" in p.stdout
+
+
+@pytest.mark.gpu
+def test_spmv_csr_dump_y_is_reference_bitwise_fp32(tmp_path):
+    out = tmp_path / "y.bin"
+    run(BUILD / "spmv-csr", GOLDEN / "lap32.mtx.rcm.csr", 3, "--dtype", "f32", "--dump-y", out)
+    y = np.fromfile(out, np.float32)
+    g = np.load(GOLDEN / "lap32.mtx.rcm.npz")
+    assert np.array_equal(y.view(np.uint32), g["y_ref_f32_ones"].view(np.uint32))
+    run(BUILD / "spmv-csr", GOLDEN / "lap32.mtx.rcm.csr", 3, "--x", "rand:42", "--dump-y", out)
+    y = np.fromfile(out, np.float64)
+    assert np.array_equal(y, g["y_orc_f64_rand"])
+
+
+@pytest.mark.gpu
+def test_spmv_csr_kernels_and_onebased():
+    for extra in (["--kernel", "vector:8"], ["--kernel", "vector"], ["--kernel", "stream", "--nt"]):
+        p = run(BUILD / "spmv-csr", GOLDEN / "lap32.onebased.csr", 4, "--x", "rand:1", *extra)
+        assert "index_base 1" in p.stdout and "Check: PASS" in p.stdout
+
+
+@pytest.mark.gpu
+def test_spmv_csrk_modes(tmp_path):
+    f = GOLDEN / "powerlaw1500.csr"
+    # manual sizes (hip/spmv.cu:112-132)
+    p = run(BUILD / "spmv-csrk", f, 5, 7, 8, "--x", "rand:3")
+    assert "using ssrs 7, srs 8" in p.stdout and "Check: PASS" in p.stdout
+    harness_parse(p.stdout)
+    # auto sizes (hip/spmv-auto-mi100.cu:130-158)
+    for params in ("mi100", "volta", "mi355x"):
+        p = run(BUILD / "spmv-csrk", f, 5, "--params", params)
+        assert "using ssrs" in p.stdout and "Number Wrong: 0" in p.stdout
+    # .csr3 input carries its own maps
+    p = run(BUILD / "spmv-csrk", GOLDEN / "powerlaw1500.csr3", 5, "--x", "rand:3")
+    assert "using ssrs" not in p.stdout and "Check: PASS" in p.stdout
+    assert "Kernel: csr3" in p.stdout
+
+
+@pytest.mark.gpu
+def test_cli_bad_input_fails_loudly(tmp_path):
+    bad = tmp_path / "bad.csr"
+    bad.write_text("2 2 2\n0 1 2\n0 7\n1.0 2.0\n")
+    p = run(BUILD / "spmv-csr", bad, 3, check=False)
+    assert p.returncode != 0 and "out of" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bin_cache_through_cli(tmp_path):
+    import hspmv
+    A = gen.stencil27(30)
+    maps = hspmv.build_csr3_maps(A, 20, 10)
+    f = tmp_path / "s.bin"
+    hspmv.save_bin(f, A, maps)
+    p = run(BUILD / "spmv-csrk", f, 5, "--x", "rand:9")
+    assert "Check: PASS" in p.stdout and "Kernel: csr3" in p.stdout
+    p = run(BUILD / "spmv-csr", f, 5, "--x", "rand:9")
+    assert "Check: PASS" in p.stdout and "Kernel: stream" in p.stdout

@@ -1,0 +1,97 @@
+"""Multi-rank row-range partition on the CPU with gloo,
+world_size 2 and 3: each rank builds only its shard, x is broadcast from rank
+0, the per-rank y (computed here by the oracle, the GPU's stand-in on a
+CPU-only box) is all-gathered, and the result must equal the oracle on the
+global matrix -- the same orchestration bench.py runs over RCCL."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, config, q):
+    sys.path.insert(0, str(REPO / "heterogeneous-spmv_amd"))
+    sys.path.insert(0, str(REPO / "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from hspmv import dist as hdist
+        from hspmv import gen
+        sh = hdist.build_shard(config, rank, world)
+        x = torch.zeros(sh.n_global, dtype=torch.float64)
+        if rank == 0:
+            x.copy_(torch.from_numpy(gen.rand_x(sh.n_global, 42)))
+        hdist.broadcast_x(x)
+        xn = x.numpy()
+        y_local = oracle.spmv(sh.A.row_ptr, sh.A.col_idx, sh.A.val, xn)
+        ok, rel = hdist.checksum_ok(sh.A, xn, y_local)
+        y = hdist.gather_y(torch.from_numpy(y_local), sh.splits).numpy()
+        nnz = torch.tensor([sh.A.nnz], dtype=torch.int64)
+        dist.all_reduce(nnz)
+        q.put((rank, y if rank == 0 else None, ok, int(nnz.item()), sh.splits.tolist(),
+               sh.nnz_global, sh.A.m))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_range_partition_gloo(world):
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle
+    from hspmv import gen
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "small", q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda r: r[0])
+    y = res[0][1]
+    A = gen.laplace2d(64, 64 * world)
+    y_ref = oracle.spmv(A.row_ptr, A.col_idx, A.val, gen.rand_x(A.n, 42))
+    assert np.array_equal(y, y_ref)
+    assert all(r[2] for r in res)                       # per-rank checksum identity
+    assert res[0][3] == A.nnz == res[0][5]              # shards cover every nonzero once
+    splits = np.array(res[0][4])
+    assert splits[0] == 0 and splits[-1] == A.m and np.all(np.diff(splits) > 0)
+    shard_nnz = A.row_ptr[splits[1:]] - A.row_ptr[splits[:-1]]
+    assert shard_nnz.max() - shard_nnz.min() <= 10     # nnz-balanced
+
+
+def test_weak_scaling_shards_have_equal_work():
+    from hspmv import dist as hdist
+    for world in (1, 2, 4, 8):
+        rows = [hdist.build_shard("small", r, world).A.m for r in range(world)]
+        assert abs(max(rows) - min(rows)) <= 64
+        assert sum(rows) == 64 * 64 * world
+
+
+def test_c4_split_is_nnz_balanced_without_building_the_matrix():
+    from hspmv import dist as hdist
+    row_nnz = hdist.banded_row_nnz(20_000_000)
+    assert 199_999_000 < row_nnz.sum() <= 200_000_000
+    s = hdist.splits_from_row_nnz(row_nnz, 8)
+    rp = np.concatenate([[0], np.cumsum(row_nnz)])
+    per = rp[s[1:]] - rp[s[:-1]]
+    assert per.max() - per.min() <= 20
