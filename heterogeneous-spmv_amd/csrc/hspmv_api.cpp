@@ -56,6 +56,13 @@ struct Shard {
   void *y = nullptr;       // y in use (own or bound)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int64_t bytes = 0;
+  // planner tables (owned): CSR-3 wave tasks and split-row chunks
+  DevPlan dp;
+  int32_t *d_task = nullptr, *d_long_row = nullptr, *d_long_cstart = nullptr,
+          *d_chunk_k = nullptr;
+  void *d_partials = nullptr;
+  // host copies kept until the plan is built
+  std::vector<int32_t> h_rp, h_outer, h_inner;
 };
 
 }  // namespace
@@ -97,6 +104,11 @@ void free_shard(Shard &s, bool borrowed) {
     (void)hipFree(s.d_outer);
     (void)hipFree(s.d_inner);
   }
+  (void)hipFree(s.d_task);
+  (void)hipFree(s.d_long_row);
+  (void)hipFree(s.d_long_cstart);
+  (void)hipFree(s.d_chunk_k);
+  (void)hipFree(s.d_partials);
   (void)hipFree(s.d_x);
   if (!s.d_yfull) (void)hipFree(s.d_y);
   (void)hipFree(s.d_yfull);
@@ -123,7 +135,8 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
   if (y_rows_alloc > 0) {
     if ((rc = dev_alloc(&s.d_y, sv * (size_t)y_rows_alloc, &s.bytes))) return rc;
   }
-  std::vector<int32_t> rp((size_t)(m + 1));
+  std::vector<int32_t> &rp = s.h_rp;
+  rp.resize((size_t)(m + 1));
   for (int64_t i = 0; i <= m; ++i) rp[i] = (int32_t)(A->row_ptr[r0 + i] - k0);
   HIP_TRY(hipMemcpy(s.d_rp, rp.data(), 4 * (size_t)(m + 1), hipMemcpyHostToDevice));
   if (nnz) {
@@ -141,7 +154,9 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
     const int64_t nssr = ssr1 - ssr0;
     const int64_t sr0 = mp->outer[ssr0], sr1 = mp->outer[ssr1];
     const int64_t nsr = sr1 - sr0;
-    std::vector<int32_t> o((size_t)(nssr + 1)), in((size_t)(nsr + 1));
+    std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
+    o.resize((size_t)(nssr + 1));
+    in.resize((size_t)(nsr + 1));
     for (int64_t i = 0; i <= nssr; ++i) o[i] = (int32_t)(mp->outer[ssr0 + i] - sr0);
     for (int64_t i = 0; i <= nsr; ++i) in[i] = (int32_t)(mp->inner[sr0 + i] - r0);
     if ((rc = dev_alloc(&s.d_outer, 4 * (size_t)(nssr + 1), &s.bytes))) return rc;
@@ -157,6 +172,72 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
   return HSPMV_OK;
 }
 
+// Host planner tables for one shard (needs s.h_rp, and s.h_outer/h_inner for
+// CSR-3):
+//  * split rows: rows longer than kLongRow, cut into kLongChunk pieces;
+//  * CSR-3 wave tasks: each super-super-row's super-rows split into
+//    waves_per_block contiguous ranges with ~equal nonzeros -- the first
+//    super-row s with rp[inner[s]] >= k0 + (k1-k0)*w/W starts wave w.
+int build_plan_tables(Shard &s, int dtype, unsigned flags) {
+  const std::vector<int32_t> &rp = s.h_rp;
+  const int64_t m = s.A.m;
+  s.dp = DevPlan();
+  if (s.plan.kernel != kVector && !(flags & HSPMV_FLAG_NO_SPLIT)) {
+    std::vector<int32_t> lrow, lcs(1, 0), ck;
+    for (int64_t r = 0; r < m; ++r) {
+      const int32_t b = rp[r], e = rp[r + 1];
+      if (e - b <= kLongRow) continue;
+      lrow.push_back((int32_t)r);
+      for (int32_t k = b; k < e; k += kLongChunk) {
+        ck.push_back(k);
+        ck.push_back(e - k > kLongChunk ? k + kLongChunk : e);
+      }
+      lcs.push_back((int32_t)(ck.size() / 2));
+    }
+    if (!lrow.empty()) {
+      int rc;
+      const int64_t nl = (int64_t)lrow.size(), nc = (int64_t)ck.size() / 2;
+      if ((rc = dev_alloc(&s.d_long_row, 4 * (size_t)nl, &s.bytes))) return rc;
+      if ((rc = dev_alloc(&s.d_long_cstart, 4 * (size_t)(nl + 1), &s.bytes))) return rc;
+      if ((rc = dev_alloc(&s.d_chunk_k, 8 * (size_t)nc, &s.bytes))) return rc;
+      if ((rc = dev_alloc(&s.d_partials, dtype_size(dtype) * (size_t)nc, &s.bytes))) return rc;
+      HIP_TRY(hipMemcpy(s.d_long_row, lrow.data(), 4 * (size_t)nl, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(s.d_long_cstart, lcs.data(), 4 * (size_t)(nl + 1), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(s.d_chunk_k, ck.data(), 8 * (size_t)nc, hipMemcpyHostToDevice));
+      s.dp.long_t = kLongRow;
+      s.dp.n_long = (int32_t)nl;
+      s.dp.n_chunks = (int32_t)nc;
+      s.dp.long_row = s.d_long_row;
+      s.dp.long_cstart = s.d_long_cstart;
+      s.dp.chunk_k = s.d_chunk_k;
+      s.dp.partials = s.d_partials;
+    }
+  }
+  if (s.plan.kernel == kCsr3) {
+    const std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
+    const int64_t nssr = s.A.n_ssr;
+    const int W = s.plan.waves_per_block;
+    std::vector<int32_t> ts((size_t)(nssr * W + 1));
+    for (int64_t b = 0; b < nssr; ++b) {
+      const int32_t s0 = o[b], s1 = o[b + 1];
+      const int64_t k0 = rp[in[s0]], k1 = rp[in[s1]];
+      int32_t sr = s0;
+      for (int w = 0; w < W; ++w) {
+        const int64_t target = k0 + (k1 - k0) * w / W;
+        while (sr < s1 && rp[in[sr]] < target) ++sr;
+        ts[(size_t)(b * W + w)] = in[w == 0 ? s0 : sr];
+      }
+    }
+    ts[(size_t)(nssr * W)] = (int32_t)m;
+    int rc;
+    if ((rc = dev_alloc(&s.d_task, 4 * ts.size(), &s.bytes))) return rc;
+    HIP_TRY(hipMemcpy(s.d_task, ts.data(), 4 * ts.size(), hipMemcpyHostToDevice));
+    s.dp.task_start = s.d_task;
+    s.dp.n_tasks = (int32_t)(nssr * W);
+  }
+  return HSPMV_OK;
+}
+
 int finish_shard(Shard &s, int dtype, unsigned flags, void *stream) {
   HIP_TRY(hipSetDevice(s.device));
   if (stream) {
@@ -168,9 +249,14 @@ int finish_shard(Shard &s, int dtype, unsigned flags, void *stream) {
   }
   HIP_TRY(hipEventCreate(&s.ev0));
   HIP_TRY(hipEventCreate(&s.ev1));
-  s.plan = plan_launch(s.A, dtype, flags, s.mean_rows_per_ssr);
+  s.plan = plan_launch(s.A, dtype, flags, s.mean_rows_per_ssr, s.h_rp.data());
+  int rc = build_plan_tables(s, dtype, flags);
+  if (rc) return rc;
   s.x = s.d_x;
   s.y = s.d_y;
+  std::vector<int32_t>().swap(s.h_rp);
+  std::vector<int32_t>().swap(s.h_outer);
+  std::vector<int32_t>().swap(s.h_inner);
   return HSPMV_OK;
 }
 
@@ -230,7 +316,8 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
         (A->dtype != HSPMV_F32 && A->dtype != HSPMV_F64) || !A->row_ptr)
       return set_error(HSPMV_E_INVALID, "bad device matrix description");
     HIP_TRY(hipSetDevice(device));
-    std::vector<int32_t> rp((size_t)(A->m + 1));
+    std::vector<int32_t> &rp = s.h_rp;
+    rp.resize((size_t)(A->m + 1));
     HIP_TRY(hipMemcpy(rp.data(), A->row_ptr, 4 * (size_t)(A->m + 1), hipMemcpyDeviceToHost));
     hspmv_csr view = *A;
     view.row_ptr = rp.data();
@@ -241,7 +328,9 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
     s.A.m = (int32_t)A->m; s.A.n = A->n; s.A.nnz = A->nnz;
     s.A.row_ptr = A->row_ptr; s.A.col_idx = A->col_idx; s.A.val = A->val;
     if (maps && maps->n_ssr > 0) {
-      std::vector<int32_t> o((size_t)(maps->n_ssr + 1)), in((size_t)(maps->n_sr + 1));
+      std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
+      o.resize((size_t)(maps->n_ssr + 1));
+      in.resize((size_t)(maps->n_sr + 1));
       HIP_TRY(hipMemcpy(o.data(), maps->outer, 4 * o.size(), hipMemcpyDeviceToHost));
       HIP_TRY(hipMemcpy(in.data(), maps->inner, 4 * in.size(), hipMemcpyDeviceToHost));
       hspmv_csr3_maps mv = {maps->n_ssr, maps->n_sr, o.data(), in.data()};
@@ -417,7 +506,7 @@ int hspmv_spmv(hspmv_handle *h) {
   if (!h->x_set) return set_error(HSPMV_E_STATE, "x not set (hspmv_set_x / hspmv_bind_x_device)");
   for (auto &s : h->shards) {
     HIP_TRY(hipSetDevice(s.device));
-    hipError_t e = launch_spmv(s.A, h->dtype, s.plan, s.x, s.y, s.stream);
+    hipError_t e = launch_spmv(s.A, s.dp, h->dtype, s.plan, s.x, s.y, s.stream);
     if (e != hipSuccess)
       return set_error(HSPMV_E_HIP, "SpMV launch on GPU %d failed: %s", s.device, hipGetErrorString(e));
   }
@@ -450,7 +539,7 @@ int hspmv_run(hspmv_handle *h, int warmup, int iters, hspmv_timing *out) {
     for (auto &s : h->shards) {
       HIP_TRY(hipSetDevice(s.device));
       HIP_TRY(hipEventRecord(s.ev0, s.stream));
-      hipError_t e = launch_spmv(s.A, h->dtype, s.plan, s.x, s.y, s.stream);
+      hipError_t e = launch_spmv(s.A, s.dp, h->dtype, s.plan, s.x, s.y, s.stream);
       if (e != hipSuccess)
         return set_error(HSPMV_E_HIP, "SpMV launch failed: %s", hipGetErrorString(e));
       HIP_TRY(hipEventRecord(s.ev1, s.stream));
@@ -541,6 +630,9 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->alg_bytes = hspmv_alg_bytes(h->m, h->n, h->nnz, h->dtype, h->n_ssr, h->n_sr);
   out->flops = 2.0 * (double)h->nnz;
   for (auto &sh : h->shards) out->device_bytes += sh.bytes;
+  out->chunk_u = s.plan.u;
+  out->n_split_rows = s.dp.n_long;
+  out->xcd_remap = s.plan.xcd_remap ? 1 : 0;
   return HSPMV_OK;
 }
 

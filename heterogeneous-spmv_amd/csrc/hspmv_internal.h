@@ -21,20 +21,52 @@ struct DevCSR {
 
 enum Kernel : int { kAuto = 0, kVector = 1, kStream = 2, kCsr3 = 3 };
 
+// Rows longer than this many nonzeros ("split rows") are cut into chunks of
+// kLongChunk nonzeros, each summed by its own workgroup, and the chunk sums
+// are added per row by a second small kernel (deterministic order).
+constexpr int32_t kLongRow = 4096;
+constexpr int32_t kLongChunk = 4096;
+
+// Device-side tables the host planner builds once per shard (all optional).
+struct DevPlan {
+  // CSR-3: wave task t covers rows [task_start[t], task_start[t+1]);
+  // waves_per_block tasks per super-super-row, nnz-balanced on super-row
+  // boundaries (the multilevel maps decide the split).
+  const int32_t *task_start = nullptr;
+  int32_t n_tasks = 0;
+  // split rows
+  int32_t long_t = 0x7fffffff;  // rows with more nonzeros are split rows
+  int32_t n_long = 0, n_chunks = 0;
+  const int32_t *long_row = nullptr;    // n_long row ids (shard-local)
+  const int32_t *long_cstart = nullptr; // n_long+1, chunk ranges per split row
+  const int32_t *chunk_k = nullptr;     // 2*n_chunks: [k0, k1) per chunk
+  void *partials = nullptr;             // n_chunks partial sums (dtype)
+};
+
 struct LaunchPlan {
   int kernel = kStream;
-  int lanes = 64;          // VECTOR: lanes per row; STREAM: rows per task
+  int lanes = 64;          // VECTOR: lanes per row; STREAM/CSR3: 64 rows per wave pass
   int waves_per_block = 4; // CSR3: waves per super-super-row workgroup
+  int u = 8;               // STREAM/CSR3: elements per lane per LDS chunk
   bool nontemporal = false;
+  bool prefetch = false;   // STREAM/CSR3: next chunk's col/val issued early
+  bool xcd_remap = true;   // contiguous row ranges per XCD (L2 reuse of x)
   int64_t blocks = 0;
 };
 
 // Chooses kernel / lanes / block shape for a shard (host-side heuristic).
-LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags,
-                       double max_ssr_rows_mean);
+// row_ptr_host: the shard's row pointer (m+1) on the host.
+LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_rows_per_ssr,
+                       const int32_t *row_ptr_host);
 
-// Enqueues one y = A*x.  Returns hipSuccess or the launch error.
-hipError_t launch_spmv(const DevCSR &A, int dtype, const LaunchPlan &plan,
+// STREAM / CSR3 row kernels (stream_f32.hip / stream_f64.hip).
+hipError_t launch_rows_f32(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p,
+                           const float *x, float *y, hipStream_t st);
+hipError_t launch_rows_f64(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p,
+                           const double *x, double *y, hipStream_t st);
+
+// Enqueues one y = A*x (main kernel + split-row kernels when present).
+hipError_t launch_spmv(const DevCSR &A, const DevPlan &dp, int dtype, const LaunchPlan &plan,
                        const void *x, void *y, hipStream_t stream);
 
 }  // namespace hspmv

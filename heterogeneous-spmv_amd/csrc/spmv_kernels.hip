@@ -6,35 +6,43 @@
 // cuda-spmv-csrk/hip/csrk.cu:185-390).  It is an HBM-bound gather: 2 flops per
 // 12 B (fp64) / 8 B (fp32) of matrix stream, so no MFMA anywhere here.
 //
-// Three kernels, all wave64-native:
+// Kernels (all wave64-native):
 //
-//  * hspmv_csr_vector<T, L>  (HSPMV_KERNEL_VECTOR)
-//      L lanes (a sub-wave, L | 64) per row, lanes stride the row's nonzeros
-//      with coalesced val/col loads and FMA, reduced by __shfl_xor inside the
-//      L-lane group.  Replaces cuda_spmv (thread per row, L = 1) and
-//      cuSpMV_3_vec's veclevel lanes + barrier-free volatile-LDS tree
-//      (csrk.cu:222-240) with a wave64-safe shuffle reduction.
-//
-//  * hspmv_csr_stream<T>     (HSPMV_KERNEL_STREAM)
+//  * hspmv_csr_stream<T, NT, U>   (HSPMV_KERNEL_STREAM, the default for CSR)
 //      one wavefront per group of 64 consecutive rows.  The group's nonzeros
 //      are contiguous, so the wave streams them with fully coalesced loads
 //      (U elements per lane per chunk), forms the products val*x[col] and
-//      stages them in a per-wave LDS slice; then lane i sums row i's products
-//      left to right.  The summation order and rounding (product rounded,
-//      then sum rounded, starting from 0) are exactly those of omp_spmv, so
-//      the result is BIT-IDENTICAL to the CPU reference.  Groups holding a
-//      row longer than kSerialMax switch to a mixed path: short rows summed in
-//      order straight from global memory (still bit-exact), long rows by the
-//      whole wave (FMA + shuffle tree: within the 1e-6 fp64 tolerance).
+//      stages them in a per-wave LDS slice.  Then
+//        - rows of <= kSerialMax nonzeros: lane i sums row i left to right.
+//          Summation order and rounding (product rounded, then sum rounded,
+//          starting from 0) are those of omp_spmv, so these rows are
+//          BIT-IDENTICAL to the CPU reference;
+//        - longer rows: the whole wave sums the row's products in the chunk
+//          (shuffle tree), accumulated over chunks (fp64 tolerance);
+//        - split rows (> kLongRow nonzeros) are skipped here and summed by
+//          hspmv_long_chunks + hspmv_long_reduce (many workgroups per row).
+//      Replaces cuda_spmv's thread-per-row scalar loop (uncoalesced) with a
+//      CSR-stream scheme (coalesced stream + LDS segmented sums).
 //
-//  * hspmv_csr3<T, W>        (HSPMV_KERNEL_CSR3)
-//      CSR-3: one workgroup of W waves per super-super-row (outer map);
-//      the workgroup's super-rows (inner map) are split between its waves by
-//      binary search on rp[inner[s]] so every wave gets ~1/W of the
-//      workgroup's nonzeros; each wave then runs the stream routine over its
-//      contiguous row range.  Replaces cuSpMV_3 / cuSpMV_3_vec (thread/
+//  * hspmv_csr3<T, NT, U, W>      (HSPMV_KERNEL_CSR3)
+//      CSR-3: one workgroup of W waves per super-super-row (outer map).  The
+//      host planner splits each super-super-row's super-rows (inner map)
+//      into W contiguous, nnz-balanced row ranges -- the multilevel maps
+//      decide where a wave's work starts -- and each wave runs the stream
+//      routine over its range.  Replaces cuSpMV_3 / cuSpMV_3_vec (thread or
 //      sub-warp per row inside (8,12)-thread blocks, csrk.cu:185-319) and
 //      cuSpMV_2 (degenerate outer level).
+//
+//  * hspmv_csr_vector<T, L, NT>   (HSPMV_KERNEL_VECTOR)
+//      L lanes (a sub-wave, L | 64) per row, lanes stride the row's nonzeros
+//      with FMA, reduced by __shfl_xor inside the L-lane group.  Replaces
+//      cuSpMV_3_vec's veclevel lanes + barrier-free volatile-LDS tree
+//      (csrk.cu:222-240) with a wave64-safe shuffle reduction; L = 1 is the
+//      thread-per-row cuda_spmv shape.
+//
+// Blocks are remapped so each of the 8 XCDs (private 4 MiB L2 each) gets a
+// contiguous range of row groups: neighbouring rows share x[] lines and the
+// edges of val/col lines, which then hit in one L2 instead of eight.
 //
 // Build: hipcc --offload-arch=gfx950 -ffp-contract=off.  Contraction is off so
 // that only the explicit fma() calls (vector kernel, long rows) fuse.
@@ -46,8 +54,6 @@ namespace hspmv {
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kSerialMax = 32;  // longest row summed serially by one lane
-constexpr int kStreamU = 8;     // elements per lane per LDS chunk
 
 template <bool NT, typename T>
 __device__ __forceinline__ T ldg(const T *p) {
@@ -57,94 +63,12 @@ __device__ __forceinline__ T ldg(const T *p) {
     return *p;
 }
 
-// Orders a wave's LDS writes before its other lanes' LDS reads (the
-// wave-scope equivalent of a barrier; no s_barrier involved).
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
   return v;
 }
-
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, kWave));
-  return v;
-}
-
-// One wavefront computes rows [g0, g1), g1 - g0 <= 64.  lds: kWave*U
-// elements private to this wave.  See the file header for the algorithm.
-template <typename T, bool NT, int U>
-__device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1,
-                                          const int32_t *__restrict__ rp,
-                                          const int32_t *__restrict__ ci,
-                                          const T *__restrict__ val,
-                                          const T *__restrict__ x,
-                                          T *__restrict__ y, T *lds, int lane) {
-  const int32_t row = g0 + lane;
-  const bool valid = row < g1;
-  const int32_t beg = valid ? rp[row] : 0;
-  const int32_t end = valid ? rp[row + 1] : 0;
-  const int32_t len = end - beg;
-  const int32_t kb = __shfl(beg, 0, kWave);
-  const int32_t ke = __shfl(end, g1 - g0 - 1, kWave);
-  const int32_t maxlen = wave_max(len);
-  T acc = T(0);
-  if (maxlen <= kSerialMax) {
-    // Ordered path: coalesced stream of the group's nonzeros through LDS.
-    for (int32_t c = kb; c < ke; c += kWave * U) {
-      const int32_t last = min(kWave * U, ke - c) - 1;
-      T prod[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        // Clamp instead of branching so every load issues back to back
-        // (a per-element predicate makes hipcc wait vmcnt(0) per element).
-        const int32_t j = min(u * kWave + lane, last);
-        const int32_t col = ldg<NT>(ci + c + j);
-        prod[u] = ldg<NT>(val + c + j) * x[col];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) lds[u * kWave + lane] = prod[u];
-      wave_sync();
-      const int32_t lo = max(beg, c);
-      const int32_t hi = min(end, c + last + 1);
-      for (int32_t k = lo; k < hi; ++k) acc = acc + lds[k - c];
-      wave_sync();
-    }
-  } else {
-    // Mixed path: short rows in order from global memory, long rows by the
-    // whole wave.
-    if (len <= kSerialMax) {
-      for (int32_t k = beg; k < end; ++k)
-        acc = acc + ldg<NT>(val + k) * x[ldg<NT>(ci + k)];
-    }
-    unsigned long long longmask = __ballot(valid && len > kSerialMax);
-    while (longmask) {
-      const int r = __ffsll(longmask) - 1;
-      longmask &= longmask - 1;
-      const int32_t rb = __shfl(beg, r, kWave);
-      const int32_t re = __shfl(end, r, kWave);
-      T s0 = T(0), s1 = T(0);
-      int32_t k = rb + lane;
-      for (; k + kWave < re; k += 2 * kWave) {
-        s0 = fma(ldg<NT>(val + k), x[ldg<NT>(ci + k)], s0);
-        s1 = fma(ldg<NT>(val + k + kWave), x[ldg<NT>(ci + k + kWave)], s1);
-      }
-      if (k < re) s0 = fma(ldg<NT>(val + k), x[ldg<NT>(ci + k)], s0);
-      const T s = wave_sum(s0 + s1);
-      if (lane == r) acc = s;
-    }
-  }
-  if (valid) y[row] = acc;
-}
-
-// ------------------------------------------------------------------ kernels
 
 template <typename T, int L, bool NT>
 __global__ __launch_bounds__(256) void hspmv_csr_vector(
@@ -165,78 +89,61 @@ __global__ __launch_bounds__(256) void hspmv_csr_vector(
   }
 }
 
-template <typename T, bool NT, int U>
-__global__ __launch_bounds__(256) void hspmv_csr_stream(
-    int32_t m, const int32_t *__restrict__ rp, const int32_t *__restrict__ ci,
-    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
-  __shared__ T lds[4 * kWave * U];
-  const int wid = threadIdx.x >> 6;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t g0 = ((int64_t)blockIdx.x * 4 + wid) * kWave;
-  if (g0 >= m) return;  // wave-uniform; no block barrier in this kernel
-  const int32_t g1 = (int32_t)min<int64_t>(g0 + kWave, m);
-  wave_rows<T, NT, U>((int32_t)g0, g1, rp, ci, val, x, y,
-                      lds + wid * kWave * U, lane);
+// Split rows, step 1: one 256-thread workgroup per chunk of <= kLongChunk
+// nonzeros of one long row -> partials[chunk].
+template <typename T, bool NT>
+__global__ __launch_bounds__(256) void hspmv_long_chunks(
+    int32_t n_chunks, const int32_t *__restrict__ chunk_k, const int32_t *__restrict__ ci,
+    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ partials) {
+  __shared__ T red[4];
+  const int c = blockIdx.x;
+  if (c >= n_chunks) return;  // block-uniform
+  const int32_t k0 = chunk_k[2 * c], k1 = chunk_k[2 * c + 1];
+  T s0 = T(0), s1 = T(0);
+  int32_t k = k0 + threadIdx.x;
+  for (; k + 256 < k1; k += 512) {
+    s0 = fma(ldg<NT>(val + k), x[ldg<NT>(ci + k)], s0);
+    s1 = fma(ldg<NT>(val + k + 256), x[ldg<NT>(ci + k + 256)], s1);
+  }
+  if (k < k1) s0 = fma(ldg<NT>(val + k), x[ldg<NT>(ci + k)], s0);
+  const T s = wave_sum(s0 + s1);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[c] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// First super-row s in [lo, hi] with rp[inner[s]] >= target (wave-uniform).
-__device__ __forceinline__ int32_t sr_lower_bound(
-    int32_t lo, int32_t hi, int64_t target, const int32_t *__restrict__ inner,
-    const int32_t *__restrict__ rp) {
-  while (lo < hi) {
-    const int32_t mid = lo + ((hi - lo) >> 1);
-    if ((int64_t)rp[inner[mid]] < target)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  return lo;
-}
-
-template <typename T, bool NT, int U, int W>
-__global__ __launch_bounds__(W * 64) void hspmv_csr3(
-    int32_t n_ssr, const int32_t *__restrict__ outer,
-    const int32_t *__restrict__ inner, const int32_t *__restrict__ rp,
-    const int32_t *__restrict__ ci, const T *__restrict__ val,
-    const T *__restrict__ x, T *__restrict__ y) {
-  __shared__ T lds[W * kWave * U];
-  const int wid = threadIdx.x >> 6;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int32_t b = blockIdx.x;
-  const int32_t s0 = outer[b];
-  const int32_t s1 = outer[b + 1];
-  int32_t sa = s0, sb = s1;
-  if constexpr (W > 1) {
-    const int64_t k0 = rp[inner[s0]];
-    const int64_t k1 = rp[inner[s1]];
-    if (wid > 0) sa = sr_lower_bound(s0, s1, k0 + (k1 - k0) * wid / W, inner, rp);
-    if (wid < W - 1)
-      sb = sr_lower_bound(s0, s1, k0 + (k1 - k0) * (wid + 1) / W, inner, rp);
-  }
-  const int32_t r0 = inner[sa];
-  const int32_t r1 = inner[sb];
-  T *my = lds + wid * kWave * U;
-  for (int32_t g0 = r0; g0 < r1; g0 += kWave)
-    wave_rows<T, NT, U>(g0, min(g0 + kWave, r1), rp, ci, val, x, y, my, lane);
+// Split rows, step 2: one wave per long row adds its chunk partials.
+template <typename T>
+__global__ __launch_bounds__(256) void hspmv_long_reduce(
+    int32_t n_long, const int32_t *__restrict__ long_row, const int32_t *__restrict__ cstart,
+    const T *__restrict__ partials, T *__restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= n_long) return;
+  const int32_t c0 = cstart[j], c1 = cstart[j + 1];
+  T s = T(0);
+  for (int32_t c = c0 + lane; c < c1; c += kWave) s += partials[c];
+  s = wave_sum(s);
+  if (lane == 0) y[long_row[j]] = s;
 }
 
 // ------------------------------------------------------------------ dispatch
 
 template <typename T, bool NT>
-hipError_t launch_typed(const DevCSR &A, const LaunchPlan &p, const T *x, T *y,
-                        hipStream_t st) {
+hipError_t launch_typed(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x,
+                        T *y, hipStream_t st) {
+  if (A.m == 0) return hipSuccess;
   const int32_t *rp = A.row_ptr;
   const int32_t *ci = A.col_idx;
   const T *val = static_cast<const T *>(A.val);
-  if (A.m == 0) return hipSuccess;
-  const dim3 grid((unsigned)p.blocks);
+  hipError_t e = hipSuccess;
   switch (p.kernel) {
     case kVector:
       switch (p.lanes) {
-#define HSPMV_VEC(L)                                                         \
-  case L:                                                                    \
-    hipLaunchKernelGGL((hspmv_csr_vector<T, L, NT>), grid, dim3(256), 0, st, \
-                       A.m, rp, ci, val, x, y);                              \
+#define HSPMV_VEC(L)                                                                    \
+  case L:                                                                               \
+    hipLaunchKernelGGL((hspmv_csr_vector<T, L, NT>), dim3((unsigned)p.blocks), dim3(256), \
+                       0, st, A.m, rp, ci, val, x, y);                                  \
     break;
         HSPMV_VEC(1) HSPMV_VEC(2) HSPMV_VEC(4) HSPMV_VEC(8) HSPMV_VEC(16)
         HSPMV_VEC(32) HSPMV_VEC(64)
@@ -244,33 +151,28 @@ hipError_t launch_typed(const DevCSR &A, const LaunchPlan &p, const T *x, T *y,
         default:
           return hipErrorInvalidValue;
       }
-      break;
+      return hipGetLastError();  // the vector kernel sums split rows itself
     case kStream:
-      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, kStreamU>), grid, dim3(256),
-                         0, st, A.m, rp, ci, val, x, y);
-      break;
     case kCsr3:
-      switch (p.waves_per_block) {
-        case 1:
-          hipLaunchKernelGGL((hspmv_csr3<T, NT, kStreamU, 1>), grid, dim3(64),
-                             0, st, A.n_ssr, A.outer, A.inner, rp, ci, val, x, y);
-          break;
-        case 2:
-          hipLaunchKernelGGL((hspmv_csr3<T, NT, kStreamU, 2>), grid, dim3(128),
-                             0, st, A.n_ssr, A.outer, A.inner, rp, ci, val, x, y);
-          break;
-        case 4:
-          hipLaunchKernelGGL((hspmv_csr3<T, NT, kStreamU, 4>), grid, dim3(256),
-                             0, st, A.n_ssr, A.outer, A.inner, rp, ci, val, x, y);
-          break;
-        default:
-          return hipErrorInvalidValue;
-      }
+      if constexpr (sizeof(T) == 8)
+        e = launch_rows_f64(A, dp, p, x, y, st);
+      else
+        e = launch_rows_f32(A, dp, p, x, y, st);
+      if (e != hipSuccess) return e;
       break;
     default:
       return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (dp.n_long > 0) {
+    hipLaunchKernelGGL((hspmv_long_chunks<T, NT>), dim3((unsigned)dp.n_chunks), dim3(256), 0, st,
+                       dp.n_chunks, dp.chunk_k, ci, val, x, static_cast<T *>(dp.partials));
+    hipLaunchKernelGGL((hspmv_long_reduce<T>), dim3((unsigned)((dp.n_long + 3) / 4)), dim3(256),
+                       0, st, dp.n_long, dp.long_row, dp.long_cstart,
+                       static_cast<const T *>(dp.partials), y);
+    e = hipGetLastError();
+  }
+  return e;
 }
 
 int floor_pow2(double v) {
@@ -279,20 +181,34 @@ int floor_pow2(double v) {
   return p;
 }
 
+// Elements per lane per LDS chunk.  Measured on MI355X (profiles/r01_sweep*):
+// the chunk must stay small enough for 8 waves/SIMD (U = 4: 62 VGPRs fp64),
+// and a 64-row group that fits one chunk of U <= 6 should be done in one.
+int pick_u(double nnz_per_pass, int dtype) {
+  if (nnz_per_pass <= 128.0) return 2;
+  if (nnz_per_pass <= 192.0) return 3;
+  if (nnz_per_pass <= 256.0) return 4;
+  if (nnz_per_pass <= 384.0) return 6;
+  return dtype == 1 ? 4 : 8;
+}
+
 }  // namespace
 
-LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags,
-                       double mean_rows_per_ssr) {
-  (void)dtype;
+LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_rows_per_ssr,
+                       const int32_t *rp_host) {
+  (void)rp_host;
   LaunchPlan p;
   const unsigned k = flags & 0xFu;
   p.nontemporal = (flags & (1u << 12)) != 0;
+  p.prefetch = (flags & (1u << 21)) != 0;  // HSPMV_FLAG_PREFETCH
+  p.xcd_remap = (flags & (1u << 14)) == 0;  // HSPMV_FLAG_NO_XCD_REMAP
   const double d = A.m ? (double)A.nnz / (double)A.m : 0.0;
   if (k == kAuto)
     p.kernel = (A.n_ssr > 0) ? kCsr3 : kStream;
   else
     p.kernel = (int)k;
   if (p.kernel == kCsr3 && A.n_ssr <= 0) p.kernel = kStream;
+  const int forced_u = (int)((flags >> 16) & 0x1Fu);  // HSPMV_U(u)
   switch (p.kernel) {
     case kVector: {
       int lanes = (int)((flags >> 4) & 0x7Fu);
@@ -307,14 +223,19 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags,
     }
     case kStream: {
       p.lanes = kWave;
+      p.u = forced_u ? forced_u : pick_u(64.0 * (d < kLongRow ? d : kLongRow), dtype);
       const int64_t tasks = ((int64_t)A.m + kWave - 1) / kWave;
       p.blocks = (tasks + 3) / 4;
       break;
     }
     case kCsr3: {
       p.lanes = kWave;
-      p.waves_per_block =
-          mean_rows_per_ssr >= 192.0 ? 4 : (mean_rows_per_ssr >= 96.0 ? 2 : 1);
+      // ~64 rows per wave: one lane per row in the ordered sums
+      const double w = mean_rows_per_ssr / 64.0;
+      p.waves_per_block = w >= 6.0 ? 8 : (w >= 3.0 ? 4 : (w >= 1.5 ? 2 : 1));
+      const double rows_per_task = mean_rows_per_ssr / p.waves_per_block;
+      const double per_pass = (rows_per_task < 64.0 ? rows_per_task : 64.0) * d;
+      p.u = forced_u ? forced_u : pick_u(per_pass < 64.0 * kLongRow ? per_pass : 64.0 * kLongRow, dtype);
       p.blocks = A.n_ssr;
       break;
     }
@@ -322,16 +243,16 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags,
   return p;
 }
 
-hipError_t launch_spmv(const DevCSR &A, int dtype, const LaunchPlan &plan,
+hipError_t launch_spmv(const DevCSR &A, const DevPlan &dp, int dtype, const LaunchPlan &plan,
                        const void *x, void *y, hipStream_t stream) {
   if (dtype == 1) {
     return plan.nontemporal
-               ? launch_typed<double, true>(A, plan, (const double *)x, (double *)y, stream)
-               : launch_typed<double, false>(A, plan, (const double *)x, (double *)y, stream);
+               ? launch_typed<double, true>(A, dp, plan, (const double *)x, (double *)y, stream)
+               : launch_typed<double, false>(A, dp, plan, (const double *)x, (double *)y, stream);
   }
   return plan.nontemporal
-             ? launch_typed<float, true>(A, plan, (const float *)x, (float *)y, stream)
-             : launch_typed<float, false>(A, plan, (const float *)x, (float *)y, stream);
+             ? launch_typed<float, true>(A, dp, plan, (const float *)x, (float *)y, stream)
+             : launch_typed<float, false>(A, dp, plan, (const float *)x, (float *)y, stream);
 }
 
 }  // namespace hspmv

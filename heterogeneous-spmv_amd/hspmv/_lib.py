@@ -21,6 +21,10 @@ KERNEL_AUTO, KERNEL_VECTOR, KERNEL_STREAM, KERNEL_CSR3 = 0, 1, 2, 3
 LANES_SHIFT = 4
 FLAG_NONTEMPORAL = 1 << 12
 FLAG_DEVICE_PTRS = 1 << 13
+FLAG_NO_XCD_REMAP = 1 << 14
+FLAG_NO_SPLIT = 1 << 15
+U_SHIFT = 16
+FLAG_PREFETCH = 1 << 21
 
 E_CODES = {0: "OK", -1: "E_INVALID", -2: "E_IO", -3: "E_NOMEM", -4: "E_HIP",
            -5: "E_RCCL", -6: "E_NODEV", -7: "E_STATE"}
@@ -68,7 +72,8 @@ class Timing(C.Structure):
 class Info(C.Structure):
     _fields_ = [("kernel", C.c_int32), ("lanes", C.c_int32), ("waves_per_block", C.c_int32),
                 ("num_gpus", C.c_int32), ("blocks", C.c_int64), ("alg_bytes", C.c_double),
-                ("flops", C.c_double), ("device_bytes", C.c_int64)]
+                ("flops", C.c_double), ("device_bytes", C.c_int64), ("chunk_u", C.c_int32),
+                ("n_split_rows", C.c_int32), ("xcd_remap", C.c_int32), ("reserved", C.c_int32)]
 
 
 _P = C.c_void_p

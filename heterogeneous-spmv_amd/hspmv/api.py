@@ -240,11 +240,21 @@ class SpMV:
 
     def __init__(self, A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, num_gpus: int = 1,
                  kernel: str = "auto", lanes: int = 0, nontemporal: bool = False,
-                 device: Optional[int] = None, stream: Optional[int] = None):
+                 device: Optional[int] = None, stream: Optional[int] = None,
+                 xcd_remap: bool = True, split_rows: bool = True, chunk_u: int = 0,
+                 prefetch: Optional[bool] = None):
         self.A = A
         self.maps = maps
         self.dtype = A.val.dtype
         flags = _KERNELS[kernel] | lanes_flag(lanes) | (FLAG_NONTEMPORAL if nontemporal else 0)
+        flags |= (0 if xcd_remap else _lib.FLAG_NO_XCD_REMAP)
+        flags |= (0 if split_rows else _lib.FLAG_NO_SPLIT)
+        if chunk_u:
+            if chunk_u not in (2, 3, 4, 6, 8, 16):
+                raise ValueError("chunk_u must be one of 2, 3, 4, 6, 8, 16")
+            flags |= chunk_u << _lib.U_SHIFT
+        if prefetch:
+            flags |= _lib.FLAG_PREFETCH
         cs = A.c_struct()
         ms = maps.c_struct() if maps is not None else None
         h = C.c_void_p()

@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Runs ONE (config, variant) SpMV for a fixed number of launches -- the
+workload under rocprofv3 --pmc / --kernel-trace passes.
+
+    python heterogeneous-spmv_amd/tools/run_one.py --config c3 --kernel stream --u 4 --iters 50
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parent))
+sys.path.insert(0, str(HERE))
+
+import hspmv  # noqa: E402
+from hspmv import gen  # noqa: E402
+from sweep import build  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--kernel", default="auto")
+    ap.add_argument("--u", type=int, default=0)
+    ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--pf", action="store_true")
+    ap.add_argument("--nt", action="store_true")
+    ap.add_argument("--noxcd", action="store_true")
+    ap.add_argument("--mi355x-maps", action="store_true")
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    A, maps, desc = build(a.config)
+    if a.kernel == "csr3" and (maps is None or a.mi355x_maps):
+        maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
+    if a.kernel != "csr3" and a.kernel != "auto":
+        maps = None
+    op = hspmv.SpMV(A, maps, kernel=a.kernel, chunk_u=a.u, lanes=a.lanes, prefetch=a.pf,
+                    nontemporal=a.nt, xcd_remap=not a.noxcd)
+    op.set_x(gen.rand_x(A.n, 42).astype(A.val.dtype))
+    t = op.run(warmup=3, iters=a.iters)
+    nssr, nsr = (maps.n_ssr, maps.n_sr) if maps is not None else (0, 0)
+    b = hspmv.alg_bytes(A.m, A.n, A.nnz, A.val.dtype, nssr, nsr)
+    print(json.dumps({"config": a.config, "desc": desc, "info": op.info, "t_min_us": t["t_min"] * 1e6,
+                      "t_avg_us": t["t_avg"] * 1e6, "alg_bytes": b,
+                      "gbps_min": b / t["t_min"] * 1e-9}))
+    op.close()
+
+
+if __name__ == "__main__":
+    main()

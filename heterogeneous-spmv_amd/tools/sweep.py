@@ -52,19 +52,28 @@ def build(cfg):
     raise ValueError(cfg)
 
 
-def variants(cfg, A, maps):
-    v = [("stream", dict(kernel="stream"), None)]
+def variants(cfg, A, maps, full=False):
+    """Kernel variants to time.  Default: the tuning grid over chunk size U,
+    prefetch and XCD remap for STREAM and CSR3, plus the VECTOR widths."""
     d = A.nnz / A.m
-    lanes = [4, 8, 16] if d < 16 else [8, 16, 32, 64]
+    v = []
+    lanes = [4, 8] if d < 16 else [16, 64]
     for L in lanes:
         v.append((f"vector{L}", dict(kernel="vector", lanes=L), None))
-    if maps is not None:
-        v.append(("csr3", dict(kernel="csr3"), maps))
-    else:
-        m2 = hspmv.build_csr3_maps(A, *hspmv.csr3_params(d, "mi355x"))
-        v.append(("csr3-mi355x", dict(kernel="csr3"), m2))
-    v += [(name + "+nt", dict(kw, nontemporal=True), mp) for name, kw, mp in list(v)
-          if name in ("stream", "csr3", "csr3-mi355x")]
+    m3 = maps if maps is not None else hspmv.build_csr3_maps(A, *hspmv.csr3_params(d, "mi355x"))
+    tag3 = "csr3" if maps is not None else "csr3-mi355x"
+    for u in (2, 3, 4, 6, 8):
+        for pf in (False, True):
+            sfx = f"-u{u}" + ("-pf" if pf else "")
+            v.append(("stream" + sfx, dict(kernel="stream", chunk_u=u, prefetch=pf), None))
+            v.append((tag3 + sfx, dict(kernel="csr3", chunk_u=u, prefetch=pf), m3))
+    v.append(("stream-auto", dict(kernel="stream"), None))
+    v.append((tag3 + "-auto", dict(kernel="csr3"), m3))
+    v.append(("stream-auto-noxcd", dict(kernel="stream", xcd_remap=False), None))
+    v.append((tag3 + "-auto-noxcd", dict(kernel="csr3", xcd_remap=False), m3))
+    v.append(("stream-auto-nt", dict(kernel="stream", nontemporal=True), None))
+    if cfg == "c5":
+        v.append(("stream-nosplit", dict(kernel="stream", split_rows=False), None))
     return v
 
 
@@ -111,7 +120,8 @@ def main():
                    "t_min_us": round(tmin * 1e6, 3), "t_avg_us": round(tmed * 1e6, 3),
                    "gbps_min": round(b / tmin * 1e-9, 1), "gbps_avg": round(b / tmed * 1e-9, 1),
                    "gflops_min": round(2 * A.nnz / tmin * 1e-9, 1), "frac_peak": round(b / tmin * 1e-9 / PEAK, 4),
-                   "desc": desc}
+                   "chunk_u": op.info["chunk_u"], "waves_per_block": op.info["waves_per_block"],
+                   "n_split_rows": op.info["n_split_rows"], "desc": desc}
             lines.append(rec)
             print(json.dumps(rec), flush=True)
             op.close()

@@ -112,6 +112,10 @@ typedef struct {
   double alg_bytes;   /* algorithmic bytes per SpMV        */
   double flops;       /* 2 * nnz                                           */
   int64_t device_bytes; /* device memory held by the handle (all GPUs)     */
+  int32_t chunk_u;    /* STREAM/CSR3 elements per lane per LDS chunk        */
+  int32_t n_split_rows; /* rows summed by the split-row kernels (GPU 0)     */
+  int32_t xcd_remap;  /* 1 = XCD-contiguous block order                    */
+  int32_t reserved;
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
@@ -131,6 +135,15 @@ typedef struct hspmv_handle hspmv_handle;
 #define HSPMV_FLAG_NONTEMPORAL (1u << 12) /* nt loads for val/col streams  */
 #define HSPMV_FLAG_DEVICE_PTRS (1u << 13) /* A/maps are device pointers on
                                              the target device (borrowed)  */
+#define HSPMV_FLAG_NO_XCD_REMAP (1u << 14) /* keep dispatch-order blocks    */
+#define HSPMV_FLAG_NO_SPLIT (1u << 15)     /* no split-row kernels: very
+                                              long rows stay on one wave   */
+/* STREAM/CSR3 elements per lane per LDS chunk: HSPMV_U(u), u in {2,3,4,6,8,16};
+ * 0 = auto from the mean row length */
+#define HSPMV_U_SHIFT 16
+#define HSPMV_U(u) ((unsigned)(u) << HSPMV_U_SHIFT)
+#define HSPMV_FLAG_PREFETCH (1u << 21) /* STREAM/CSR3: software-pipelined
+                                          col/val loads one chunk ahead   */
 
 /* ---------------------------------------------------------------- handle */
 /* Upload A (and optional CSR-3 maps) to num_gpus devices (0 = all visible).

@@ -232,3 +232,54 @@ def test_config_c5_powerlaw_csr3_fp32():
     nrow = np.diff(A.row_ptr)
     err = np.abs(y.astype(np.float64) - y32.astype(np.float64))
     assert np.all(err <= (nrow + 2) * 2.0 ** -23 * absrow + 1e-30)
+
+
+def _split_row_matrix(seed=3):
+    """Rows of 5e3 .. 1.2e5 nonzeros (split rows) beside short and medium rows,
+    including split rows first, last, adjacent, and at 64-row group edges."""
+    rng = np.random.default_rng(seed)
+    m, n = 700, 150_000
+    lens = rng.integers(0, 40, m)
+    lens[rng.integers(0, m, 40)] = rng.integers(33, 4000, 40)     # medium rows
+    for r, ln in [(0, 120_000), (1, 4097), (63, 5000), (64, 9000), (65, 4096), (300, 30_000),
+                  (301, 70_000), (699, 8193)]:
+        lens[r] = ln
+    rp = np.concatenate([[0], np.cumsum(lens)])
+    ci = np.concatenate([np.sort(rng.choice(n, ln, replace=False)) for ln in lens])
+    return hspmv.CsrMatrix(m, n, rp, ci, rng.uniform(-1, 1, rp[-1]))
+
+
+def test_split_rows_all_kernels():
+    A = _split_row_matrix()
+    x = gen.rand_x(A.n, 4)
+    lens = np.diff(A.row_ptr)
+    maps = hspmv.build_csr3_maps(A, 20, 4)
+    for kw, mp in [(dict(kernel="stream"), None), (dict(kernel="auto"), maps),
+                   (dict(kernel="stream", split_rows=False), None),
+                   (dict(kernel="csr3", split_rows=False), maps),
+                   (dict(kernel="stream", xcd_remap=False), None),
+                   (dict(kernel="vector", lanes=64), None)]:
+        y, info = gpu_spmv(A, x, mp, **kw)
+        split = kw.get("split_rows", True) and kw["kernel"] != "vector"
+        assert info["n_split_rows"] == (int((lens > 4096).sum()) if split else 0), kw
+        check_fp64(A, x, y, exact_rows=short_rows(A) if kw["kernel"] != "vector" else None)
+
+
+def test_chunk_u_and_remap_variants():
+    for A in (gen.stencil27(24), gen.powerlaw(40000, seed=21, dtype=np.float64)):
+        x = gen.rand_x(A.n, 6)
+        ys = []
+        maps = hspmv.build_csr3_maps(A, 20, 10)
+        for u in (2, 3, 4, 6, 8, 16):
+            for remap, pf in ((True, False), (False, True), (True, True)):
+                y, info = gpu_spmv(A, x, kernel="stream", chunk_u=u, xcd_remap=remap, prefetch=pf)
+                assert info["chunk_u"] == u and info["xcd_remap"] == int(remap)
+                ys.append(y)
+                y3, _ = gpu_spmv(A, x, maps, chunk_u=u, xcd_remap=remap, prefetch=pf)
+                ys.append(y3)
+        ok = short_rows(A)
+        y64 = check_fp64(A, x, ys[0], exact_rows=ok)
+        absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+        for y in ys[1:]:
+            assert np.array_equal(y[ok], ys[0][ok])
+            assert fp64_tol_ok(y, y64, absrow)
