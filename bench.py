@@ -216,7 +216,7 @@ def main():
         del yfull
 
     flops_step = 2.0 * shard.nnz_global
-    alg_local = hspmv.alg_bytes(A.m, A.n, A.nnz, dtype)
+    alg_local = info["alg_bytes"]  # x counted as the distinct columns this shard reads
     alg_total = sum_over_ranks(alg_local, world)
     gflops = flops_step / step_s * 1e-9
     achieved = alg_local / ev_launch_s * 1e-9

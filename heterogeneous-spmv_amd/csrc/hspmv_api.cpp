@@ -56,6 +56,7 @@ struct Shard {
   void *y = nullptr;       // y in use (own or bound)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int64_t bytes = 0;
+  int64_t x_entries = 0;   // distinct columns of this shard
   // planner tables (owned): CSR-3 wave tasks and split-row chunks
   DevPlan dp;
   int32_t *d_task = nullptr, *d_long_row = nullptr, *d_long_cstart = nullptr,
@@ -77,6 +78,11 @@ struct hspmv_handle {
   bool x_set = false;
   bool borrowed = false;  // HSPMV_FLAG_DEVICE_PTRS: matrix arrays not owned
   int64_t max_rows = 0;   // multi-GPU padding for the y all-gather
+  int64_t x_entries() const {
+    int64_t t = 0;
+    for (auto &s : shards) t += s.x_entries;
+    return t;
+  }
   std::vector<ncclComm_t> comms;
 };
 
@@ -118,6 +124,15 @@ void free_shard(Shard &s, bool borrowed) {
   s = Shard();
 }
 
+// Number of distinct column indices in col[0..nnz) (< n): x entries read.
+int64_t count_distinct_cols(const int32_t *col, int64_t nnz, int64_t n) {
+  std::vector<uint64_t> bits((size_t)(n / 64 + 1), 0);
+  for (int64_t k = 0; k < nnz; ++k) bits[(size_t)col[k] >> 6] |= 1ull << (col[k] & 63);
+  int64_t c = 0;
+  for (uint64_t w : bits) c += __builtin_popcountll(w);
+  return c;
+}
+
 // Uploads rows [r0, r1) of A (and the matching slice of the maps) to shard s.
 int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_t r0, int64_t r1,
                  int64_t ssr0, int64_t ssr1, int64_t y_rows_alloc) {
@@ -139,6 +154,7 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
   rp.resize((size_t)(m + 1));
   for (int64_t i = 0; i <= m; ++i) rp[i] = (int32_t)(A->row_ptr[r0 + i] - k0);
   HIP_TRY(hipMemcpy(s.d_rp, rp.data(), 4 * (size_t)(m + 1), hipMemcpyHostToDevice));
+  s.x_entries = count_distinct_cols(A->col_idx + k0, nnz, A->n);
   if (nnz) {
     HIP_TRY(hipMemcpy(s.d_ci, A->col_idx + k0, 4 * (size_t)nnz, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(s.d_val, (const char *)A->val + sv * k0, sv * (size_t)nnz,
@@ -319,14 +335,19 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
     std::vector<int32_t> &rp = s.h_rp;
     rp.resize((size_t)(A->m + 1));
     HIP_TRY(hipMemcpy(rp.data(), A->row_ptr, 4 * (size_t)(A->m + 1), hipMemcpyDeviceToHost));
-    hspmv_csr view = *A;
+    hspmv_csr view = *A;  // device col/val are only null-checked, never read here
     view.row_ptr = rp.data();
-    view.col_idx = nullptr;
-    view.val = nullptr;
-    if (A->nnz > 0 && (!A->col_idx || !A->val)) return set_error(HSPMV_E_INVALID, "col/val NULL");
-    if ((rc = validate_host_csr(&view, false)) != HSPMV_OK && A->nnz > 0) return rc;
+    if ((rc = validate_host_csr(&view, false)) != HSPMV_OK) return rc;
     s.A.m = (int32_t)A->m; s.A.n = A->n; s.A.nnz = A->nnz;
     s.A.row_ptr = A->row_ptr; s.A.col_idx = A->col_idx; s.A.val = A->val;
+    {
+      std::vector<int32_t> cols((size_t)A->nnz);
+      if (A->nnz)
+        HIP_TRY(hipMemcpy(cols.data(), A->col_idx, 4 * (size_t)A->nnz, hipMemcpyDeviceToHost));
+      for (int32_t c : cols)
+        if (c < 0 || c >= A->n) return set_error(HSPMV_E_INVALID, "device col_idx %d out of [0, %lld)", c, (long long)A->n);
+      s.x_entries = count_distinct_cols(cols.data(), A->nnz, A->n);
+    }
     if (maps && maps->n_ssr > 0) {
       std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
       o.resize((size_t)(maps->n_ssr + 1));
@@ -560,7 +581,7 @@ int hspmv_run(hspmv_handle *h, int warmup, int iters, hspmv_timing *out) {
   out->t_min = tmin; out->t_max = tmax; out->t_avg = tsum / iters;
   out->wall_min = wmin; out->wall_max = wmax; out->wall_avg = wsum / iters;
   out->gflops = tmin > 0 ? 2.0 * (double)h->nnz / tmin * 1e-9 : 0.0;
-  out->gbps_alg = tmin > 0 ? hspmv_alg_bytes(h->m, h->n, h->nnz, h->dtype, h->n_ssr, h->n_sr) / tmin * 1e-9 : 0.0;
+  out->gbps_alg = tmin > 0 ? hspmv_alg_bytes(h->m, h->x_entries(), h->nnz, h->dtype, h->n_ssr, h->n_sr) / tmin * 1e-9 : 0.0;
   out->iters = iters;
   out->num_gpus = (int32_t)h->shards.size();
   return HSPMV_OK;
@@ -627,7 +648,8 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->waves_per_block = s.plan.waves_per_block;
   out->num_gpus = (int32_t)h->shards.size();
   out->blocks = s.plan.blocks;
-  out->alg_bytes = hspmv_alg_bytes(h->m, h->n, h->nnz, h->dtype, h->n_ssr, h->n_sr);
+  out->x_entries = h->x_entries();
+  out->alg_bytes = hspmv_alg_bytes(h->m, out->x_entries, h->nnz, h->dtype, h->n_ssr, h->n_sr);
   out->flops = 2.0 * (double)h->nnz;
   for (auto &sh : h->shards) out->device_bytes += sh.bytes;
   out->chunk_u = s.plan.u;

@@ -10,6 +10,12 @@
 namespace hspmv {
 namespace dev {
 
+// Ablation builds only (make diag): 1 = skip the ordered row sums, 2 = skip
+// the x gather (x[col] := 1), 3 = both.  Results are wrong in those builds.
+#ifndef HSPMV_DIAG
+#define HSPMV_DIAG 0
+#endif
+
 constexpr int kWave = 64;
 constexpr int kSerialMax = 32;  // longest row summed serially by one lane
 constexpr int kNumXcd = 8;
@@ -50,27 +56,53 @@ __device__ __forceinline__ unsigned long long bits_from(int i) {
   return i >= 64 ? 0ull : (~0ull << i);
 }
 
-// One chunk's col/val registers (U per lane, lane-strided => coalesced).
-template <typename T, bool NT, int U>
-struct Chunk {
-  int32_t col[U];
-  T v[U];
-  // Loads elements [c, c+64U) clamped to c+last (clamp, not branch: a
-  // per-element predicate makes hipcc wait vmcnt(0) per element).
-  __device__ __forceinline__ void load(const int32_t *__restrict__ ci, const T *__restrict__ val,
-                                       int32_t c, int32_t last, int lane) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int32_t j = min(u * kWave + lane, last);
-      col[u] = ldg<NT>(ci + c + j);
-      v[u] = ldg<NT>(val + c + j);
-    }
+// Loads through a wave-uniform GLOBAL (address_space 1) base pointer plus a
+// 32-bit byte offset, so hipcc emits global_load ... v_off, s[base:base+1]
+// (one offset VGPR per load, no 64-bit address pairs, and no flat_load,
+// which would force vmcnt(0) + lgkmcnt(0) waits).
+typedef __attribute__((address_space(1))) const char gchar;
+
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_off(const gchar *base, uint32_t byte_off) {
+  const __attribute__((address_space(1))) T *p =
+      (const __attribute__((address_space(1))) T *)(base + byte_off);
+  if constexpr (NT)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+
+template <typename T>
+__device__ __forceinline__ const gchar *uniform_ptr(const T *p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const gchar *)(((uint64_t)hi << 32) | lo);
+}
+
+// Ordered sum of lds[lo..hi) into acc, left to right: the LDS reads are
+// issued 4 at a time (one LDS latency per 4 nonzeros instead of per nonzero)
+// but the additions stay in sequence, so the rounding is omp_spmv's.
+template <typename T>
+__device__ __forceinline__ T ordered_sum(T acc, const T *lds, int32_t lo, int32_t hi) {
+  int32_t k = lo;
+  for (; k + 4 <= hi; k += 4) {
+    const T a0 = lds[k], a1 = lds[k + 1], a2 = lds[k + 2], a3 = lds[k + 3];
+    acc = acc + a0;
+    acc = acc + a1;
+    acc = acc + a2;
+    acc = acc + a3;
   }
-};
+  for (; k < hi; ++k) acc = acc + lds[k];
+  return acc;
+}
 
 // One wavefront computes rows [g0, g1), g1 - g0 <= 64.  lds: kWave*U
-// elements private to this wave.  PF: software-pipelined -- the next chunk's
-// col/val loads are issued before this chunk's LDS sums.
+// elements private to this wave.  Per chunk of 64*U nonzeros: stage A loads
+// col/val (coalesced), stage B gathers x[col], stage C forms the products
+// into LDS; then the row sums.  PF (software pipelining): the next chunk's
+// stage A is issued between this chunk's stage B and C, so its latency
+// overlaps the gather and the sums.
 template <typename T, bool NT, int U, bool PF>
 __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t long_t,
                                           const int32_t *__restrict__ rp,
@@ -87,6 +119,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t long_t
   const unsigned long long skipmask = __ballot(valid && skip);
   const unsigned long long coopmask = __ballot(valid && !skip && len > kSerialMax);
   const bool serial = valid && !skip && len <= kSerialMax;
+  const gchar *xb = uniform_ptr(x);
   T acc = T(0);
   // Runs of consecutive non-split rows [a, b); normally one run = the group.
   int32_t a = g0;
@@ -94,33 +127,53 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t long_t
     const unsigned long long rest = skipmask & bits_from(a - g0);
     const int32_t b = rest ? g0 + (__ffsll(rest) - 1) : g1;
     if (b > a) {
-      const int32_t kb = __shfl(beg, a - g0, kWave);
-      const int32_t ke = __shfl(end, b - 1 - g0, kWave);
+      const int32_t kb = __builtin_amdgcn_readfirstlane(__shfl(beg, a - g0, kWave));
+      const int32_t ke = __builtin_amdgcn_readfirstlane(__shfl(end, b - 1 - g0, kWave));
+      const int32_t n_run = ke - kb;
+      const gchar *cb = uniform_ptr(ci + kb);
+      const gchar *vb = uniform_ptr(val + kb);
       const unsigned long long coop = coopmask & bits_from(a - g0) & ~bits_from(b - g0);
       const bool mine = serial && row >= a && row < b;
-      Chunk<T, NT, U> ch;
-      if constexpr (PF) {
-        if (kb < ke) ch.load(ci, val, kb, min(kWave * U, ke - kb) - 1, lane);
-      }
-      for (int32_t c = kb; c < ke; c += kWave * U) {
-        const int32_t last = min(kWave * U, ke - c) - 1;
-        if constexpr (!PF) ch.load(ci, val, c, last, lane);
-        T prod[U];
+      int32_t col[U];
+      T v[U];
+      auto stage_a = [&](int32_t c0, int32_t last) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) prod[u] = ch.v[u] * x[ch.col[u]];
+        for (int u = 0; u < U; ++u) {
+          // clamp instead of branching: every load issues back to back
+          const uint32_t j = (uint32_t)(c0 + min(u * kWave + lane, last));
+          col[u] = ld_off<NT, int32_t>(cb, j * 4u);
+          v[u] = ld_off<NT, T>(vb, j * (uint32_t)sizeof(T));
+        }
+      };
+      if constexpr (PF) {
+        if (n_run > 0) stage_a(0, min(kWave * U, n_run) - 1);
+      }
+      for (int32_t c0 = 0; c0 < n_run; c0 += kWave * U) {
+        const int32_t last = min(kWave * U, n_run - c0) - 1;
+        if constexpr (!PF) stage_a(c0, last);
+        T xv[U], vv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if constexpr ((HSPMV_DIAG & 2) != 0)
+            xv[u] = T(col[u] & 1) + T(1);
+          else
+            xv[u] = ld_off<false, T>(xb, (uint32_t)col[u] * (uint32_t)sizeof(T));
+          vv[u] = v[u];
+        }
         if constexpr (PF) {
-          // next chunk (clamped to the run's last element when there is none)
-          const int32_t cn = c + kWave * U;
-          const int32_t cc = cn < ke ? cn : ke - 1;
-          ch.load(ci, val, cc, cn < ke ? min(kWave * U, ke - cn) - 1 : 0, lane);
+          __builtin_amdgcn_sched_barrier(0);
+          const int32_t cn = c0 + kWave * U;
+          stage_a(cn < n_run ? cn : n_run - 1, cn < n_run ? min(kWave * U, n_run - cn) - 1 : 0);
+          __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) lds[u * kWave + lane] = prod[u];
+        for (int u = 0; u < U; ++u) lds[u * kWave + lane] = vv[u] * xv[u];
         wave_sync();
-        if (mine) {
-          const int32_t lo = max(beg, c);
-          const int32_t hi = min(end, c + last + 1);
-          for (int32_t k = lo; k < hi; ++k) acc = acc + lds[k - c];
+        const int32_t c = kb + c0;
+        if constexpr ((HSPMV_DIAG & 1) != 0) {
+          if (mine && max(beg, c) < min(end, c + last + 1)) acc += lds[max(beg, c) - c];
+        } else {
+          if (mine) acc = ordered_sum(acc, lds - c, max(beg, c), min(end, c + last + 1));
         }
         unsigned long long cm = coop;
         while (cm) {

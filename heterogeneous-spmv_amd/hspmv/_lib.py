@@ -73,7 +73,8 @@ class Info(C.Structure):
     _fields_ = [("kernel", C.c_int32), ("lanes", C.c_int32), ("waves_per_block", C.c_int32),
                 ("num_gpus", C.c_int32), ("blocks", C.c_int64), ("alg_bytes", C.c_double),
                 ("flops", C.c_double), ("device_bytes", C.c_int64), ("chunk_u", C.c_int32),
-                ("n_split_rows", C.c_int32), ("xcd_remap", C.c_int32), ("reserved", C.c_int32)]
+                ("n_split_rows", C.c_int32), ("xcd_remap", C.c_int32), ("reserved", C.c_int32),
+                ("x_entries", C.c_int64)]
 
 
 _P = C.c_void_p

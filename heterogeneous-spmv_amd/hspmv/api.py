@@ -268,6 +268,29 @@ class SpMV:
         check(rc, "hspmv_create")
         self._h = h
 
+    @classmethod
+    def from_device(cls, csr_dev: "_lib.Csr", maps_dev: "Optional[_lib.Csr3Maps]", A_meta: CsrMatrix,
+                    *, device: int = 0, stream: Optional[int] = None, kernel: str = "auto",
+                    lanes: int = 0, nontemporal: bool = False, xcd_remap: bool = True,
+                    split_rows: bool = True, chunk_u: int = 0,
+                    prefetch: Optional[bool] = None) -> "SpMV":
+        """Handle over caller-owned DEVICE arrays (HSPMV_FLAG_DEVICE_PTRS):
+        csr_dev/maps_dev hold device pointers; A_meta supplies m, n, dtype."""
+        self = cls.__new__(cls)
+        self.A = A_meta
+        self.maps = None
+        self.dtype = A_meta.val.dtype
+        flags = (_KERNELS[kernel] | lanes_flag(lanes) | (FLAG_NONTEMPORAL if nontemporal else 0)
+                 | FLAG_DEVICE_PTRS | (0 if xcd_remap else _lib.FLAG_NO_XCD_REMAP)
+                 | (0 if split_rows else _lib.FLAG_NO_SPLIT) | (chunk_u << _lib.U_SHIFT)
+                 | (_lib.FLAG_PREFETCH if prefetch else 0))
+        h = C.c_void_p()
+        check(lib().hspmv_create_on_device(C.byref(h), C.byref(csr_dev),
+                                           C.byref(maps_dev) if maps_dev is not None else None,
+                                           int(device), stream, flags), "hspmv_create_on_device")
+        self._h = h
+        return self
+
     # -- vectors
     def set_x(self, x: np.ndarray) -> None:
         x = np.ascontiguousarray(x, dtype=self.dtype)

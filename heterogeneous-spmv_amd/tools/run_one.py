@@ -39,8 +39,7 @@ def main():
                     nontemporal=a.nt, xcd_remap=not a.noxcd)
     op.set_x(gen.rand_x(A.n, 42).astype(A.val.dtype))
     t = op.run(warmup=3, iters=a.iters)
-    nssr, nsr = (maps.n_ssr, maps.n_sr) if maps is not None else (0, 0)
-    b = hspmv.alg_bytes(A.m, A.n, A.nnz, A.val.dtype, nssr, nsr)
+    b = op.info["alg_bytes"]  # x counted as the distinct columns read
     print(json.dumps({"config": a.config, "desc": desc, "info": op.info, "t_min_us": t["t_min"] * 1e6,
                       "t_avg_us": t["t_avg"] * 1e6, "alg_bytes": b,
                       "gbps_min": b / t["t_min"] * 1e-9}))

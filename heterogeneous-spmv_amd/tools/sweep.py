@@ -27,6 +27,8 @@ REPO = HERE.parent.parent
 sys.path.insert(0, str(HERE.parent))
 sys.path.insert(0, str(REPO / "oracle"))
 
+import torch  # noqa: E402,F401  (device arrays shared by all variants)
+
 import hspmv  # noqa: E402
 from hspmv import dist as hdist  # noqa: E402
 from hspmv import gen  # noqa: E402
@@ -45,11 +47,51 @@ def build(cfg):
     if cfg == "c4":
         sh = hdist.build_shard("c4", 0, 8)
         return sh.A, None, "C4 banded 2e7 rows, rank-0 shard of 8 (2.5M rows) fp64"
+    if cfg == "b27":  # diagnostic: C3's row length with a C4-like (local) gather
+        A = gen.banded(1_953_125, per_row=27, half=32, seed=5)
+        return A, None, "diag: banded 1.95M rows, 27 nnz/row within +-32, fp64"
+    if cfg == "s27n":  # diagnostic: C3's stencil in natural (non-RCM) order
+        A = gen.stencil27(125, rcm=False)
+        return A, None, "diag: 27-pt 125^3 natural order fp64"
     if cfg == "c5":
         A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32)
         maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
         return A, maps, "C5 power-law 2e6 rows CSR-3 fp32"
     raise ValueError(cfg)
+
+
+class DeviceMatrix:
+    """One device copy of A (+ x, y) in torch tensors; handles borrow it."""
+
+    def __init__(self, A, x):
+        import torch
+        self.torch = torch
+        self.A = A
+        self.rp = torch.from_numpy(A.row_ptr).cuda()
+        self.ci = torch.from_numpy(A.col_idx).cuda()
+        self.val = torch.from_numpy(A.val).cuda()
+        self.x = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+        self.y = torch.empty(A.m, dtype=self.val.dtype, device="cuda")
+        self.maps = {}
+
+    def spmv(self, maps, **kw):
+        torch = self.torch
+        meta = hspmv.CsrMatrix(self.A.m, self.A.n, np.zeros(1, np.int32), np.zeros(0, np.int32),
+                               np.zeros(0, self.A.val.dtype))
+        cs = hspmv._lib.Csr(self.A.m, self.A.n, self.A.nnz, self.rp.data_ptr(), self.ci.data_ptr(),
+                            self.val.data_ptr(), hspmv.api.dtype_code(self.A.val.dtype))
+        mdev = None
+        if maps is not None:
+            key = id(maps)
+            if key not in self.maps:
+                self.maps[key] = (torch.from_numpy(maps.outer).cuda(),
+                                  torch.from_numpy(maps.inner).cuda(), maps)
+            o, i, _ = self.maps[key]
+            mdev = hspmv._lib.Csr3Maps(maps.n_ssr, maps.n_sr, o.data_ptr(), i.data_ptr())
+        op = hspmv.SpMV.from_device(cs, mdev, meta, device=0, **kw)
+        op.bind_x_device(self.x.data_ptr())
+        op.bind_y_device(self.y.data_ptr())
+        return op
 
 
 def variants(cfg, A, maps, full=False):
@@ -83,6 +125,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--out", default="")
+    ap.add_argument("--quick", action="store_true", help="only stream u4/u6 + csr3 auto")
     a = ap.parse_args()
     import oracle
     lines = []
@@ -95,11 +138,18 @@ def main():
         print(f"# {cfg}: {desc} m={A.m} nnz={A.nnz} built in {time.time() - t0:.1f}s",
               file=sys.stderr, flush=True)
         ops = []
-        for name, kw, mp in variants(cfg, A, maps):
-            op = hspmv.SpMV(A, mp, **kw)
-            op.set_x(x)
+        vs = variants(cfg, A, maps)
+        if a.quick:
+            vs = [v for v in vs if v[0] in ("stream-u4", "stream-u6", "stream-u8", "stream-auto",
+                                          "stream-auto-noxcd", "csr3-auto", "csr3-mi355x-auto")]
+        # every variant reads the SAME device arrays (borrowed pointers), so
+        # the comparison is not skewed by where each copy was allocated
+        dev = DeviceMatrix(A, x)
+        for name, kw, mp in vs:
+            op = dev.spmv(mp, **kw)
             op.spmv()
-            y = op.get_y()
+            op.synchronize()
+            y = dev.y.cpu().numpy()
             err = np.abs(y.astype(np.float64) - y_ref.astype(np.float64))
             tol = (1e-6 if A.val.dtype == np.float64 else 1e-4) * np.abs(y_ref) + \
                   (1e-12 if A.val.dtype == np.float64 else 1e-5) * absrow
@@ -114,7 +164,7 @@ def main():
             tmin = min(t[0] for t in times[name])
             tmed = float(np.median([t[1] for t in times[name]]))
             nssr, nsr = (mp.n_ssr, mp.n_sr) if mp is not None else (0, 0)
-            b = hspmv.alg_bytes(A.m, A.n, A.nnz, A.val.dtype, nssr, nsr)
+            b = op.info["alg_bytes"]  # x counted as the distinct columns read
             rec = {"config": cfg, "variant": name, "ok": ok, "m": A.m, "nnz": A.nnz,
                    "dtype": str(A.val.dtype), "kernel": op.info["kernel_name"],
                    "t_min_us": round(tmin * 1e6, 3), "t_avg_us": round(tmed * 1e6, 3),

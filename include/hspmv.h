@@ -116,6 +116,8 @@ typedef struct {
   int32_t n_split_rows; /* rows summed by the split-row kernels (GPU 0)     */
   int32_t xcd_remap;  /* 1 = XCD-contiguous block order                    */
   int32_t reserved;
+  int64_t x_entries;  /* distinct columns referenced = x entries one SpMV
+                         must read (summed over GPUs); alg_bytes uses it    */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
@@ -230,7 +232,10 @@ int hspmv_partition_rows(int64_t m, const int32_t *row_ptr,
                          const hspmv_csr3_maps *maps, int parts,
                          int64_t *splits);
 /* Algorithmic bytes of one SpMV:
- * nnz*(sv+4) + (m+1)*4 + n*sv + m*sv (+ (n_ssr+1 + n_sr+1)*4 for CSR-3). */
+ * nnz*(sv+4) + (m+1)*4 + n*sv + m*sv (+ (n_ssr+1 + n_sr+1)*4 for CSR-3),
+ * where n = the x entries the SpMV reads, i.e. the number of distinct
+ * columns (the matrix width when every column holds a nonzero; much less for
+ * a row-range shard of a banded matrix -- hspmv_info.x_entries). */
 double hspmv_alg_bytes(int64_t m, int64_t n, int64_t nnz, int dtype,
                        int64_t n_ssr, int64_t n_sr);
 int hspmv_device_count(int *count);

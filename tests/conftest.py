@@ -11,6 +11,11 @@ from pathlib import Path
 import numpy as np
 import pytest
 
+# torch (ROCm 7.0 wheel) and libhspmv (linked against /opt/rocm 7.2) share the
+# libamdhip64.so.7 SONAME: whichever loads first serves both.  torch only works
+# with its own copy, so load torch before any test touches libhspmv.
+import torch  # noqa: F401
+
 REPO = Path(__file__).resolve().parent.parent
 GOLDEN = REPO / "tests" / "golden"
 sys.path.insert(0, str(REPO / "heterogeneous-spmv_amd"))

@@ -283,3 +283,29 @@ def test_chunk_u_and_remap_variants():
         for y in ys[1:]:
             assert np.array_equal(y[ok], ys[0][ok])
             assert fp64_tol_ok(y, y64, absrow)
+
+
+def test_borrowed_device_arrays():
+    """HSPMV_FLAG_DEVICE_PTRS: the handle reads caller-owned device arrays
+    (torch tensors here) and caller-bound x / y."""
+    import torch
+    A = gen.stencil27(30)
+    maps = hspmv.build_csr3_maps(A, 20, 10)
+    x = gen.rand_x(A.n, 13)
+    rp, ci, val = (torch.from_numpy(a).cuda() for a in (A.row_ptr, A.col_idx, A.val))
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.zeros(A.m, dtype=torch.float64, device="cuda")
+    o, i = torch.from_numpy(maps.outer).cuda(), torch.from_numpy(maps.inner).cuda()
+    cs = hspmv._lib.Csr(A.m, A.n, A.nnz, rp.data_ptr(), ci.data_ptr(), val.data_ptr(), 1)
+    ms = hspmv._lib.Csr3Maps(maps.n_ssr, maps.n_sr, o.data_ptr(), i.data_ptr())
+    for mdev, kernel in ((None, "stream"), (ms, "csr3"), (None, "vector")):
+        op = hspmv.SpMV.from_device(cs, mdev, A, device=0, kernel=kernel)
+        op.bind_x_device(xd.data_ptr())
+        op.bind_y_device(yd.data_ptr())
+        op.spmv()
+        op.synchronize()
+        check_fp64(A, x, yd.cpu().numpy(), exact_rows=short_rows(A) if kernel != "vector" else None)
+        op.close()
+    bad = hspmv._lib.Csr(A.m, A.n, A.nnz, rp.data_ptr(), 0, val.data_ptr(), 1)
+    with pytest.raises(hspmv.HspmvError, match="E_INVALID"):
+        hspmv.SpMV.from_device(bad, None, A, device=0)
