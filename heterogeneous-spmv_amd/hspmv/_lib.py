@@ -25,9 +25,17 @@ FLAG_NO_XCD_REMAP = 1 << 14
 FLAG_NO_SPLIT = 1 << 15
 U_SHIFT = 16
 FLAG_PREFETCH = 1 << 21
+FLAG_XCD_REMAP = 1 << 22
 
 E_CODES = {0: "OK", -1: "E_INVALID", -2: "E_IO", -3: "E_NOMEM", -4: "E_HIP",
            -5: "E_RCCL", -6: "E_NODEV", -7: "E_STATE"}
+
+
+def remap_flag(xcd_remap) -> int:
+    """None = library default (remap when the matrix fits the Infinity Cache)."""
+    if xcd_remap is None:
+        return 0
+    return FLAG_XCD_REMAP if xcd_remap else FLAG_NO_XCD_REMAP
 
 
 def lanes_flag(lanes: int) -> int:

@@ -23,7 +23,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import (F32, F64, KERNEL_AUTO, KERNEL_CSR3, KERNEL_STREAM, KERNEL_VECTOR,
-                   FLAG_DEVICE_PTRS, FLAG_NONTEMPORAL, HspmvError, check, lanes_flag, lib)
+                   FLAG_DEVICE_PTRS, FLAG_NONTEMPORAL, HspmvError, check, lanes_flag, lib,
+                   remap_flag)
 
 _KERNELS = {"auto": KERNEL_AUTO, "vector": KERNEL_VECTOR, "stream": KERNEL_STREAM,
             "csr3": KERNEL_CSR3}
@@ -241,13 +242,13 @@ class SpMV:
     def __init__(self, A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, num_gpus: int = 1,
                  kernel: str = "auto", lanes: int = 0, nontemporal: bool = False,
                  device: Optional[int] = None, stream: Optional[int] = None,
-                 xcd_remap: bool = True, split_rows: bool = True, chunk_u: int = 0,
+                 xcd_remap: Optional[bool] = None, split_rows: bool = True, chunk_u: int = 0,
                  prefetch: Optional[bool] = None):
         self.A = A
         self.maps = maps
         self.dtype = A.val.dtype
         flags = _KERNELS[kernel] | lanes_flag(lanes) | (FLAG_NONTEMPORAL if nontemporal else 0)
-        flags |= (0 if xcd_remap else _lib.FLAG_NO_XCD_REMAP)
+        flags |= remap_flag(xcd_remap)
         flags |= (0 if split_rows else _lib.FLAG_NO_SPLIT)
         if chunk_u:
             if chunk_u not in (2, 3, 4, 6, 8, 16):
@@ -271,7 +272,7 @@ class SpMV:
     @classmethod
     def from_device(cls, csr_dev: "_lib.Csr", maps_dev: "Optional[_lib.Csr3Maps]", A_meta: CsrMatrix,
                     *, device: int = 0, stream: Optional[int] = None, kernel: str = "auto",
-                    lanes: int = 0, nontemporal: bool = False, xcd_remap: bool = True,
+                    lanes: int = 0, nontemporal: bool = False, xcd_remap: Optional[bool] = None,
                     split_rows: bool = True, chunk_u: int = 0,
                     prefetch: Optional[bool] = None) -> "SpMV":
         """Handle over caller-owned DEVICE arrays (HSPMV_FLAG_DEVICE_PTRS):
@@ -281,7 +282,7 @@ class SpMV:
         self.maps = None
         self.dtype = A_meta.val.dtype
         flags = (_KERNELS[kernel] | lanes_flag(lanes) | (FLAG_NONTEMPORAL if nontemporal else 0)
-                 | FLAG_DEVICE_PTRS | (0 if xcd_remap else _lib.FLAG_NO_XCD_REMAP)
+                 | FLAG_DEVICE_PTRS | remap_flag(xcd_remap)
                  | (0 if split_rows else _lib.FLAG_NO_SPLIT) | (chunk_u << _lib.U_SHIFT)
                  | (_lib.FLAG_PREFETCH if prefetch else 0))
         h = C.c_void_p()

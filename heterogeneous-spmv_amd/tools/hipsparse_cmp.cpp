@@ -1,0 +1,204 @@
+// hipsparse_cmp.cpp -- external comparison point: the
+// vendor hipSPARSE SpMV (hipsparseSpMV, CSR, 32-bit indices, base zero, the
+// setup of hipsparse-spmv/spmv.cu:151-180 but our own code) timed beside the
+// libhspmv kernels on the SAME device arrays and the same x, with y compared.
+//
+//   hipsparse_cmp <matrix.bin> [iters]      (binary cache from hspmv_save_bin)
+//
+// Prints one JSON line per (algorithm): kernel-time min / median (HIP events
+// around each call, 5 warm-ups), algorithmic GB/s (x counted as distinct
+// columns, as libhspmv does), and max |y_hipsparse - y_hspmv| relative to
+// sum|a x| per row.
+#include <hip/hip_runtime.h>
+#include <hipsparse/hipsparse.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "hspmv.h"
+
+#define HIPCK(x)                                                                \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                   \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+#define SPCK(x)                                                                 \
+  do {                                                                          \
+    hipsparseStatus_t s_ = (x);                                                 \
+    if (s_ != HIPSPARSE_STATUS_SUCCESS) {                                       \
+      fprintf(stderr, "%s: status %d\n", #x, (int)s_);                          \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+static void fill_x(std::vector<double> &x, unsigned long long seed) {
+  unsigned long long s = seed;
+  for (auto &v : x) {
+    unsigned long long z = (s += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    v = (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+  }
+}
+
+int main(int argc, char **argv) {
+  if (argc < 2) {
+    fprintf(stderr, "usage: %s matrix.bin [iters]\n", argv[0]);
+    return 1;
+  }
+  const int iters = argc > 2 ? atoi(argv[2]) : 30;
+  hspmv_csr_buf A;
+  hspmv_csr3_buf maps;
+  if (hspmv_load_bin(argv[1], &A, &maps) != HSPMV_OK) {
+    fprintf(stderr, "load: %s\n", hspmv_last_error());
+    return 1;
+  }
+  const bool f64 = A.dtype == HSPMV_F64;
+  const size_t sv = f64 ? 8 : 4;
+  std::vector<double> x64((size_t)A.n);
+  fill_x(x64, 42);
+  std::vector<float> x32(x64.begin(), x64.end());
+  const void *xh = f64 ? (const void *)x64.data() : (const void *)x32.data();
+
+  int32_t *d_rp, *d_ci;
+  void *d_val, *d_x, *d_y, *d_y2;
+  HIPCK(hipMalloc(&d_rp, 4 * (A.m + 1)));
+  HIPCK(hipMalloc(&d_ci, 4 * (A.nnz ? A.nnz : 1)));
+  HIPCK(hipMalloc(&d_val, sv * (A.nnz ? A.nnz : 1)));
+  HIPCK(hipMalloc(&d_x, sv * A.n));
+  HIPCK(hipMalloc(&d_y, sv * A.m));
+  HIPCK(hipMalloc(&d_y2, sv * A.m));
+  HIPCK(hipMemcpy(d_rp, A.row_ptr, 4 * (A.m + 1), hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(d_ci, A.col_idx, 4 * A.nnz, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(d_val, A.val, sv * A.nnz, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(d_x, xh, sv * A.n, hipMemcpyHostToDevice));
+  hipStream_t st;
+  HIPCK(hipStreamCreate(&st));
+
+  // libhspmv on the same device arrays (borrowed)
+  hspmv_csr dv = {A.m, A.n, A.nnz, d_rp, d_ci, d_val, A.dtype};
+  hspmv_handle *h = nullptr;
+  if (hspmv_create_on_device(&h, &dv, nullptr, 0, st, HSPMV_FLAG_DEVICE_PTRS) != HSPMV_OK) {
+    fprintf(stderr, "hspmv: %s\n", hspmv_last_error());
+    return 1;
+  }
+  hspmv_bind_x_device(h, d_x);
+  hspmv_bind_y_device(h, d_y2);
+  hspmv_info info;
+  hspmv_get_info(h, &info);
+  const double alg = info.alg_bytes;
+
+  hipsparseHandle_t sp;
+  SPCK(hipsparseCreate(&sp));
+  SPCK(hipsparseSetStream(sp, st));
+  const hipDataType dt = f64 ? HIP_R_64F : HIP_R_32F;
+  hipsparseSpMatDescr_t mat;
+  hipsparseDnVecDescr_t vx, vy;
+  SPCK(hipsparseCreateCsr(&mat, A.m, A.n, A.nnz, d_rp, d_ci, d_val, HIPSPARSE_INDEX_32I,
+                          HIPSPARSE_INDEX_32I, HIPSPARSE_INDEX_BASE_ZERO, dt));
+  SPCK(hipsparseCreateDnVec(&vx, A.n, d_x, dt));
+  SPCK(hipsparseCreateDnVec(&vy, A.m, d_y, dt));
+  const double one64 = 1.0, zero64 = 0.0;
+  const float one32 = 1.f, zero32 = 0.f;
+  const void *alpha = f64 ? (const void *)&one64 : (const void *)&one32;
+  const void *beta = f64 ? (const void *)&zero64 : (const void *)&zero32;
+
+  hipEvent_t e0, e1;
+  HIPCK(hipEventCreate(&e0));
+  HIPCK(hipEventCreate(&e1));
+  auto timed = [&](auto launch) {
+    for (int i = 0; i < 5; ++i) launch();
+    std::vector<double> t;
+    for (int i = 0; i < iters; ++i) {
+      HIPCK(hipEventRecord(e0, st));
+      launch();
+      HIPCK(hipEventRecord(e1, st));
+      HIPCK(hipEventSynchronize(e1));
+      float ms;
+      HIPCK(hipEventElapsedTime(&ms, e0, e1));
+      t.push_back(ms * 1e-3);
+    }
+    std::sort(t.begin(), t.end());
+    return std::make_pair(t[0], t[t.size() / 2]);
+  };
+
+  // libhspmv reference timing + y
+  auto th = timed([&] { hspmv_spmv(h); });
+  std::vector<char> yh(sv * A.m), ys(sv * A.m);
+  HIPCK(hipStreamSynchronize(st));
+  HIPCK(hipMemcpy(yh.data(), d_y2, sv * A.m, hipMemcpyDeviceToHost));
+  static const char *kn[] = {"auto", "vector", "stream", "csr3"};
+  printf("{\"impl\": \"hspmv\", \"kernel\": \"%s\", \"chunk_u\": %d, \"m\": %lld, \"nnz\": %lld, "
+         "\"dtype\": \"%s\", \"t_min_us\": %.3f, \"t_med_us\": %.3f, \"gbps_min\": %.1f}\n",
+         kn[info.kernel & 3], info.chunk_u, (long long)A.m, (long long)A.nnz, f64 ? "f64" : "f32",
+         th.first * 1e6, th.second * 1e6, alg / th.first * 1e-9);
+  fflush(stdout);
+
+  // per-row |a x| sums for the comparison
+  std::vector<double> absrow((size_t)A.m, 0.0);
+  for (int64_t r = 0; r < A.m; ++r)
+    for (int32_t k = A.row_ptr[r]; k < A.row_ptr[r + 1]; ++k) {
+      const double v = f64 ? ((double *)A.val)[k] : (double)((float *)A.val)[k];
+      absrow[r] += fabs(v * x64[A.col_idx[k]]);
+    }
+
+  const struct {
+    hipsparseSpMVAlg_t alg;
+    const char *name;
+  } algs[] = {{HIPSPARSE_SPMV_ALG_DEFAULT, "default"},
+              {HIPSPARSE_SPMV_CSR_ALG1, "csr_alg1"},
+              {HIPSPARSE_SPMV_CSR_ALG2, "csr_alg2"}};
+  for (auto &a : algs) {
+    size_t bsz = 0;
+    if (hipsparseSpMV_bufferSize(sp, HIPSPARSE_OPERATION_NON_TRANSPOSE, alpha, mat, vx, beta, vy, dt,
+                                 a.alg, &bsz) != HIPSPARSE_STATUS_SUCCESS) {
+      printf("{\"impl\": \"hipsparse\", \"alg\": \"%s\", \"error\": \"bufferSize\"}\n", a.name);
+      continue;
+    }
+    void *buf = nullptr;
+    if (bsz) HIPCK(hipMalloc(&buf, bsz));  // rocSPARSE rejects a buffer when it asked for none
+    // preprocess is optional (analysis for the adaptive CSR kernels); report
+    // its status rather than aborting when this hipSPARSE build refuses it
+    const hipsparseStatus_t pst = hipsparseSpMV_preprocess(
+        sp, HIPSPARSE_OPERATION_NON_TRANSPOSE, alpha, mat, vx, beta, vy, dt, a.alg, buf);
+    const hipsparseStatus_t rst = hipsparseSpMV(sp, HIPSPARSE_OPERATION_NON_TRANSPOSE, alpha, mat,
+                                                vx, beta, vy, dt, a.alg, buf);
+    if (rst != HIPSPARSE_STATUS_SUCCESS) {
+      printf("{\"impl\": \"hipsparse\", \"alg\": \"%s\", \"buffer\": %zu, \"preprocess_status\": %d, "
+             "\"spmv_status\": %d}\n", a.name, bsz, (int)pst, (int)rst);
+      if (buf) HIPCK(hipFree(buf));
+      continue;
+    }
+    auto tt = timed([&] {
+      SPCK(hipsparseSpMV(sp, HIPSPARSE_OPERATION_NON_TRANSPOSE, alpha, mat, vx, beta, vy, dt, a.alg,
+                         buf));
+    });
+    HIPCK(hipStreamSynchronize(st));
+    HIPCK(hipMemcpy(ys.data(), d_y, sv * A.m, hipMemcpyDeviceToHost));
+    double maxrel = 0.0;
+    for (int64_t r = 0; r < A.m; ++r) {
+      const double a1 = f64 ? ((double *)yh.data())[r] : ((float *)yh.data())[r];
+      const double a2 = f64 ? ((double *)ys.data())[r] : ((float *)ys.data())[r];
+      const double rel = fabs(a1 - a2) / (absrow[r] + 1e-300);
+      if (absrow[r] > 0 && rel > maxrel) maxrel = rel;
+    }
+    printf("{\"impl\": \"hipsparse\", \"alg\": \"%s\", \"m\": %lld, \"nnz\": %lld, \"dtype\": \"%s\", "
+           "\"t_min_us\": %.3f, \"t_med_us\": %.3f, \"gbps_min\": %.1f, \"hspmv_speedup\": %.3f, "
+           "\"max_rel_diff_vs_hspmv\": %.3e, \"preprocess_status\": %d}\n",
+           a.name, (long long)A.m, (long long)A.nnz, f64 ? "f64" : "f32", tt.first * 1e6,
+           tt.second * 1e6, alg / tt.first * 1e-9, tt.first / th.first, maxrel, (int)pst);
+    fflush(stdout);
+    if (buf) HIPCK(hipFree(buf));
+  }
+  hspmv_destroy(h);
+  hipsparseDestroy(sp);
+  return 0;
+}

@@ -113,6 +113,8 @@ def variants(cfg, A, maps, full=False):
     v.append((tag3 + "-auto", dict(kernel="csr3"), m3))
     v.append(("stream-auto-noxcd", dict(kernel="stream", xcd_remap=False), None))
     v.append((tag3 + "-auto-noxcd", dict(kernel="csr3", xcd_remap=False), m3))
+    v.append(("stream-auto-xcd", dict(kernel="stream", xcd_remap=True), None))
+    v.append((tag3 + "-auto-xcd", dict(kernel="csr3", xcd_remap=True), m3))
     v.append(("stream-auto-nt", dict(kernel="stream", nontemporal=True), None))
     if cfg == "c5":
         v.append(("stream-nosplit", dict(kernel="stream", split_rows=False), None))

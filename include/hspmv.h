@@ -138,6 +138,9 @@ typedef struct hspmv_handle hspmv_handle;
 #define HSPMV_FLAG_DEVICE_PTRS (1u << 13) /* A/maps are device pointers on
                                              the target device (borrowed)  */
 #define HSPMV_FLAG_NO_XCD_REMAP (1u << 14) /* keep dispatch-order blocks    */
+/* Default (neither XCD flag): remap only when the matrix's bytes fit the
+ * 256 MiB Infinity Cache (<= 192 MiB), where per-XCD L2 reuse of x pays;
+ * HBM-resident matrices stream faster in dispatch order (profiles/r01_sweep*). */
 #define HSPMV_FLAG_NO_SPLIT (1u << 15)     /* no split-row kernels: very
                                               long rows stay on one wave   */
 /* STREAM/CSR3 elements per lane per LDS chunk: HSPMV_U(u), u in {2,3,4,6,8,16};
@@ -146,6 +149,8 @@ typedef struct hspmv_handle hspmv_handle;
 #define HSPMV_U(u) ((unsigned)(u) << HSPMV_U_SHIFT)
 #define HSPMV_FLAG_PREFETCH (1u << 21) /* STREAM/CSR3: software-pipelined
                                           col/val loads one chunk ahead   */
+#define HSPMV_FLAG_XCD_REMAP (1u << 22) /* force the XCD-contiguous block
+                                           order whatever the size         */
 
 /* ---------------------------------------------------------------- handle */
 /* Upload A (and optional CSR-3 maps) to num_gpus devices (0 = all visible).
