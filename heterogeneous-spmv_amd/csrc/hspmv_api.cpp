@@ -654,7 +654,8 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   for (auto &sh : h->shards) out->device_bytes += sh.bytes;
   out->chunk_u = s.plan.u;
   out->n_split_rows = s.dp.n_long;
-  out->xcd_remap = s.plan.xcd_remap ? 1 : 0;
+  out->xcd_remap = s.plan.xcd_chunk;
+  out->groups_per_wave = s.plan.kernel == kStream ? s.plan.groups : 1;
   return HSPMV_OK;
 }
 

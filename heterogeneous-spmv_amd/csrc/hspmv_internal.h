@@ -50,7 +50,8 @@ struct LaunchPlan {
   int u = 8;               // STREAM/CSR3: elements per lane per LDS chunk
   bool nontemporal = false;
   bool prefetch = false;   // STREAM/CSR3: next chunk's col/val issued early
-  bool xcd_remap = true;   // contiguous row ranges per XCD (L2 reuse of x)
+  int32_t xcd_chunk = 1;   // blocks per XCD turn (1 = dispatch order; see xcd_chunk_remap)
+  int32_t groups = 1;      // STREAM: 64-row groups per wave (next group's rp prefetched)
   int64_t blocks = 0;
 };
 

@@ -16,6 +16,30 @@ namespace dev {
 #define HSPMV_DIAG 0
 #endif
 
+// HSPMV_DIAG & 8: per-wave phase timestamps (s_memtime) of the STREAM
+// kernel into g_trace (read back by hspmv_diag_trace, stream_f64.hip).  Each
+// stamp first waits for all of the wave's outstanding loads, so the traced
+// build measures a serialised wave; results are correct.
+constexpr int kTraceWaves = 1 << 17;
+constexpr int kTraceSlots = 8;
+#if (HSPMV_DIAG & 8)
+static __device__ unsigned long long g_trace[kTraceWaves * kTraceSlots];
+__device__ __forceinline__ unsigned long long diag_stamp() {
+  unsigned long long t;
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)"
+               : "=s"(t)::"memory");
+  return t;
+}
+#define HSPMV_TRACE(ts, i, v)            \
+  do {                                   \
+    if ((ts) != nullptr && lane == 0) (ts)[i] = (v); \
+  } while (0)
+#else
+#define HSPMV_TRACE(ts, i, v) \
+  do {                        \
+  } while (0)
+#endif
+
 constexpr int kWave = 64;
 constexpr int kSerialMax = 32;  // longest row summed serially by one lane
 constexpr int kNumXcd = 8;
@@ -43,13 +67,20 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
-// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
-// bijective"): blocks b and b+8 share an XCD under round-robin dispatch, so
-// give XCD slot x = b % 8 the contiguous logical range of its q (+1) blocks.
-__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
-  const int64_t q = nb / kNumXcd, r = nb % kNumXcd;
-  const int64_t x = b % kNumXcd, i = b / kNumXcd;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+// Bijective XCD-aware block order (cdna_hip_programming.md §5 "XCD swizzle
+// must be bijective").  Blocks b and b+8 share an XCD under round-robin
+// dispatch; with chunk s > 1 each XCD takes s consecutive logical blocks in
+// turn, so at any moment the 8 XCDs work on 8 adjacent runs of s blocks:
+// s = nb/8 gives each XCD one contiguous eighth of the rows (x stays in
+// that XCD's L2), small s keeps the whole chip's read front compact (HBM
+// page locality) while rows still share x lines within an XCD.  s <= 1 is
+// the dispatch order.  Blocks past the last full 8*s span keep their index.
+__device__ __forceinline__ uint32_t xcd_chunk_remap(uint32_t b, uint32_t nb, uint32_t s) {
+  if (s <= 1) return b;
+  const uint32_t span = kNumXcd * s;
+  if (b >= (nb / span) * span) return b;
+  const uint32_t i = b / kNumXcd, x = b % kNumXcd;
+  return (i / s) * span + x * s + (i % s);
 }
 
 __device__ __forceinline__ unsigned long long bits_from(int i) {
@@ -97,24 +128,36 @@ __device__ __forceinline__ T ordered_sum(T acc, const T *lds, int32_t lo, int32_
   return acc;
 }
 
-// One wavefront computes rows [g0, g1), g1 - g0 <= 64.  lds: kWave*U
-// elements private to this wave.  Per chunk of 64*U nonzeros: stage A loads
-// col/val (coalesced), stage B gathers x[col], stage C forms the products
-// into LDS; then the row sums.  PF (software pipelining): the next chunk's
-// stage A is issued between this chunk's stage B and C, so its latency
-// overlaps the gather and the sums.
+// Row bounds of a 64-row group for this lane (0, 0 past g1).  Issued one
+// group ahead by the kernels, so a wave's next col/val loads never wait on
+// a row-pointer round trip.
+__device__ __forceinline__ void group_bounds(const int32_t *__restrict__ rp, int32_t g0,
+                                             int32_t g1, int lane, int32_t &beg, int32_t &end) {
+  const int32_t row = g0 + lane;
+  const bool valid = row < g1;
+  beg = valid ? rp[row] : 0;
+  end = valid ? rp[row + 1] : 0;
+}
+
+// One wavefront computes rows [g0, g1), g1 - g0 <= 64, whose bounds
+// (group_bounds) are in beg/end.  lds: kWave*U elements private to this
+// wave.  Per chunk of 64*U nonzeros: stage A loads col/val (coalesced),
+// stage B gathers x[col], stage C forms the products into LDS; then the row
+// sums.  PF (software pipelining): the next chunk's stage A is issued
+// between this chunk's stage B and C, so its latency overlaps the gather and
+// the sums.
 template <typename T, bool NT, int U, bool PF>
-__device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t long_t,
-                                          const int32_t *__restrict__ rp,
+__device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, int32_t end,
+                                          int32_t long_t,
                                           const int32_t *__restrict__ ci,
                                           const T *__restrict__ val,
                                           const T *__restrict__ x,
-                                          T *__restrict__ y, T *lds, int lane) {
+                                          T *__restrict__ y, T *lds, int lane,
+                                          unsigned long long *ts = nullptr) {
   const int32_t row = g0 + lane;
   const bool valid = row < g1;
-  const int32_t beg = valid ? rp[row] : 0;
-  const int32_t end = valid ? rp[row + 1] : 0;
   const int32_t len = end - beg;
+  (void)ts;
   const bool skip = len > long_t;
   const unsigned long long skipmask = __ballot(valid && skip);
   const unsigned long long coopmask = __ballot(valid && !skip && len > kSerialMax);
@@ -130,12 +173,15 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t long_t
       const int32_t kb = __builtin_amdgcn_readfirstlane(__shfl(beg, a - g0, kWave));
       const int32_t ke = __builtin_amdgcn_readfirstlane(__shfl(end, b - 1 - g0, kWave));
       const int32_t n_run = ke - kb;
-      const gchar *cb = uniform_ptr(ci + kb);
-      const gchar *vb = uniform_ptr(val + kb);
       const unsigned long long coop = coopmask & bits_from(a - g0) & ~bits_from(b - g0);
       const bool mine = serial && row >= a && row < b;
       int32_t col[U];
       T v[U];
+      const gchar *cb = uniform_ptr(ci + kb);
+      const gchar *vb = uniform_ptr(val + kb);
+      // (A raw-buffer form -- SGPR descriptors bounded to the run, no
+      // clamp VALU -- measured 0-2.5 % slower in one-process A/B runs,
+      // tools/ab.py, profiles/r01_ab_buffer_loads.jsonl.)
       auto stage_a = [&](int32_t c0, int32_t last) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -151,6 +197,9 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t long_t
       for (int32_t c0 = 0; c0 < n_run; c0 += kWave * U) {
         const int32_t last = min(kWave * U, n_run - c0) - 1;
         if constexpr (!PF) stage_a(c0, last);
+#if (HSPMV_DIAG & 8)
+        if (c0 == 0) HSPMV_TRACE(ts, 2, diag_stamp());
+#endif
         T xv[U], vv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -166,6 +215,9 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t long_t
           stage_a(cn < n_run ? cn : n_run - 1, cn < n_run ? min(kWave * U, n_run - cn) - 1 : 0);
           __builtin_amdgcn_sched_barrier(0);
         }
+#if (HSPMV_DIAG & 8)
+        if (c0 == 0) HSPMV_TRACE(ts, 3, diag_stamp());
+#endif
 #pragma unroll
         for (int u = 0; u < U; ++u) lds[u * kWave + lane] = vv[u] * xv[u];
         wave_sync();
@@ -189,45 +241,90 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t long_t
           }
         }
         wave_sync();
+#if (HSPMV_DIAG & 8)
+        if (c0 == 0) HSPMV_TRACE(ts, 4, diag_stamp());
+        if (c0 + kWave * U >= n_run) HSPMV_TRACE(ts, 7, (unsigned long long)(c0 / (kWave * U) + 1));
+#endif
       }
     }
     a = b + 1;
   }
+#if (HSPMV_DIAG & 8)
+  HSPMV_TRACE(ts, 5, diag_stamp());
+#endif
   if (valid && !skip) y[row] = acc;
 }
 
+// STREAM: wave w walks `groups` consecutive 64-row groups starting at row
+// w * groups * 64, loading the next group's row pointers before streaming
+// the current one.
 template <typename T, bool NT, int U, bool PF>
 __global__ __launch_bounds__(256) void hspmv_csr_stream(
-    int32_t m, int32_t long_t, int32_t remap, const int32_t *__restrict__ rp,
-    const int32_t *__restrict__ ci, const T *__restrict__ val, const T *__restrict__ x,
-    T *__restrict__ y) {
+    int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups,
+    const int32_t *__restrict__ rp, const int32_t *__restrict__ ci, const T *__restrict__ val,
+    const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[4 * kWave * U];
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t blk = remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-  const int64_t g0 = (blk * 4 + wid) * kWave;
+  const int64_t blk = xcd_chunk_remap(blockIdx.x, gridDim.x, xcd_chunk);
+  int64_t g0 = (blk * 4 + wid) * (int64_t)groups * kWave;
   if (g0 >= m) return;  // wave-uniform; no block barrier in this kernel
-  const int32_t g1 = (int32_t)min<int64_t>(g0 + kWave, m);
-  wave_rows<T, NT, U, PF>((int32_t)g0, g1, long_t, rp, ci, val, x, y, lds + wid * kWave * U,
-                          lane);
+  const int64_t gend = min<int64_t>(g0 + (int64_t)groups * kWave, m);
+  T *my = lds + wid * kWave * U;
+  unsigned long long *ts = nullptr;
+#if (HSPMV_DIAG & 8)
+  const int64_t wv = blk * 4 + wid;
+  if (wv < kTraceWaves) ts = g_trace + wv * kTraceSlots;
+  HSPMV_TRACE(ts, 0, diag_stamp());
+  {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    HSPMV_TRACE(ts, 6, (unsigned long long)hw);
+  }
+#endif
+  int32_t beg, end;
+  group_bounds(rp, (int32_t)g0, (int32_t)min<int64_t>(g0 + kWave, gend), lane, beg, end);
+#if (HSPMV_DIAG & 8)
+  HSPMV_TRACE(ts, 1, diag_stamp());
+#endif
+  while (true) {
+    const int32_t g1 = (int32_t)min<int64_t>(g0 + kWave, gend);
+    int32_t nbeg = 0, nend = 0;
+    if (g1 < gend) group_bounds(rp, g1, (int32_t)min<int64_t>(g1 + kWave, gend), lane, nbeg, nend);
+    wave_rows<T, NT, U, PF>((int32_t)g0, g1, beg, end, long_t, ci, val, x, y, my, lane, ts);
+    ts = nullptr;  // trace the first group only
+    if (g1 >= gend) break;
+    g0 = g1;
+    beg = nbeg;
+    end = nend;
+  }
 }
 
 template <typename T, bool NT, int U, bool PF, int W>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
-    int32_t n_tasks, int32_t long_t, int32_t remap, const int32_t *__restrict__ task_start,
+    int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, const int32_t *__restrict__ task_start,
     const int32_t *__restrict__ rp, const int32_t *__restrict__ ci, const T *__restrict__ val,
     const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[W * kWave * U];
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t blk = remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int64_t blk = xcd_chunk_remap(blockIdx.x, gridDim.x, xcd_chunk);
   const int64_t t = blk * W + wid;
   if (t >= n_tasks) return;
   const int32_t r0 = task_start[t];
   const int32_t r1 = task_start[t + 1];
+  if (r0 >= r1) return;
   T *my = lds + wid * kWave * U;
-  for (int32_t g0 = r0; g0 < r1; g0 += kWave)
-    wave_rows<T, NT, U, PF>(g0, min(g0 + kWave, r1), long_t, rp, ci, val, x, y, my, lane);
+  int32_t beg, end;
+  group_bounds(rp, r0, min(r0 + kWave, r1), lane, beg, end);
+  for (int32_t g0 = r0; g0 < r1; g0 += kWave) {
+    const int32_t g1 = min(g0 + kWave, r1);
+    int32_t nbeg = 0, nend = 0;
+    if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
+    wave_rows<T, NT, U, PF>(g0, g1, beg, end, long_t, ci, val, x, y, my, lane);
+    beg = nbeg;
+    end = nend;
+  }
 }
 
 // ------------------------------------------------------------------ launchers
@@ -238,12 +335,12 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
   const T *val = static_cast<const T *>(A.val);
   if (p.kernel == kStream) {
     hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF>), dim3((unsigned)p.blocks), dim3(256), 0,
-                       st, A.m, dp.long_t, (int32_t)p.xcd_remap, A.row_ptr, A.col_idx, val, x, y);
+                       st, A.m, dp.long_t, (uint32_t)p.xcd_chunk, (int32_t)p.groups, A.row_ptr, A.col_idx, val, x, y);
     return;
   }
 #define HSPMV_CSR3(W)                                                                        \
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, W>), dim3((unsigned)p.blocks), dim3(W * 64), 0, \
-                     st, dp.n_tasks, dp.long_t, (int32_t)p.xcd_remap, dp.task_start,          \
+                     st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk, dp.task_start,                \
                      A.row_ptr, A.col_idx, val, x, y)
   switch (p.waves_per_block) {
     case 1: HSPMV_CSR3(1); break;

@@ -202,19 +202,25 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_r
   p.nontemporal = (flags & (1u << 12)) != 0;
   p.prefetch = (flags & (1u << 21)) != 0;  // HSPMV_FLAG_PREFETCH
   const double d = A.m ? (double)A.nnz / (double)A.m : 0.0;
-  // XCD remap: contiguous row ranges per XCD keep x in that XCD's L2, which
-  // pays when the matrix is served from the Infinity Cache; from HBM the
-  // dispatch order (the whole chip on one compact window) streams 3-8 %
-  // faster (profiles/r01_sweep2/3: C2 remap 15.6 vs 16.9 us; C3 132 vs 128,
-  // C4 70.6 vs 65.4).
+  // XCD block order: a contiguous eighth of the rows per XCD keeps x in that
+  // XCD's L2, which pays when the matrix is served from the Infinity Cache;
+  // from HBM the dispatch order (the whole chip on one compact window)
+  // streams 3-8 % faster (profiles/r01_sweep2-4: C2 full remap 15.6 vs
+  // 16.9 us; C3 132 vs 128, C4 70.6 vs 65.4).  Chunked orders in between:
+  // xcd_chunk_remap in spmv_device.cuh.
   const double sv = dtype == 1 ? 8.0 : 4.0;
   const double footprint = (double)A.nnz * (sv + 4.0) + (double)A.m * (sv + 4.0) + (double)A.n * sv;
-  if (flags & (1u << 14))  // HSPMV_FLAG_NO_XCD_REMAP
-    p.xcd_remap = false;
+  const unsigned chunk_code = (flags >> 24) & 0x1Fu;  // HSPMV_XCD_CHUNK(s)
+  bool full = false;
+  int32_t chunk = 1;
+  if (chunk_code)
+    chunk = 1 << (chunk_code - 1);
+  else if (flags & (1u << 14))  // HSPMV_FLAG_NO_XCD_REMAP
+    chunk = 1;
   else if (flags & (1u << 22))  // HSPMV_FLAG_XCD_REMAP
-    p.xcd_remap = true;
+    full = true;
   else
-    p.xcd_remap = footprint <= 192.0 * 1024 * 1024;
+    full = footprint <= 192.0 * 1024 * 1024;
   if (k == kAuto)
     p.kernel = (A.n_ssr > 0) ? kCsr3 : kStream;
   else
@@ -237,7 +243,10 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_r
       p.lanes = kWave;
       p.u = forced_u ? forced_u : pick_u(64.0 * (d < kLongRow ? d : kLongRow), dtype);
       const int64_t tasks = ((int64_t)A.m + kWave - 1) / kWave;
-      p.blocks = (tasks + 3) / 4;
+      const unsigned gcode = (flags >> 29) & 0x7u;  // HSPMV_GROUPS(g)
+      p.groups = gcode ? 1 << (gcode - 1) : 1;
+      const int64_t waves = (tasks + p.groups - 1) / p.groups;
+      p.blocks = (waves + 3) / 4;
       break;
     }
     case kCsr3: {
@@ -252,6 +261,15 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_r
       break;
     }
   }
+  if (p.kernel == kVector) {
+    full = false;
+    chunk = 1;  // the vector kernel keeps dispatch order
+  }
+  if (full) {
+    const int64_t per_xcd = p.blocks / 8;
+    chunk = per_xcd > 1 ? (int32_t)per_xcd : 1;
+  }
+  p.xcd_chunk = chunk;
   return p;
 }
 

@@ -8,3 +8,25 @@ hipError_t launch_rows_f64(const DevCSR &A, const DevPlan &dp, const LaunchPlan 
   return dev::launch_rows<double>(A, dp, p, x, y, st);
 }
 }  // namespace hspmv
+
+#if (HSPMV_DIAG & 8)
+// Diagnostic builds only: copies the STREAM fp64 kernel's per-wave phase
+// stamps (kTraceWaves x kTraceSlots u64) to host memory `dst`.
+extern "C" int hspmv_diag_trace(void *dst, size_t bytes) {
+  const size_t n = sizeof(unsigned long long) * hspmv::dev::kTraceWaves * hspmv::dev::kTraceSlots;
+  if (bytes < n) return -1;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(hspmv::dev::g_trace), n, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? 0
+             : -4;
+}
+extern "C" int hspmv_diag_trace_clear() {
+  static unsigned long long zero[1024];
+  const size_t n = sizeof(unsigned long long) * hspmv::dev::kTraceWaves * hspmv::dev::kTraceSlots;
+  for (size_t off = 0; off < n; off += sizeof(zero))
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hspmv::dev::g_trace), zero, sizeof(zero), off,
+                          hipMemcpyHostToDevice) != hipSuccess)
+      return -4;
+  return 0;
+}
+#endif

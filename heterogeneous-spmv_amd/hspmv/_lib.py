@@ -26,16 +26,33 @@ FLAG_NO_SPLIT = 1 << 15
 U_SHIFT = 16
 FLAG_PREFETCH = 1 << 21
 FLAG_XCD_REMAP = 1 << 22
+XCD_CHUNK_SHIFT = 24
+GROUPS_SHIFT = 29
 
 E_CODES = {0: "OK", -1: "E_INVALID", -2: "E_IO", -3: "E_NOMEM", -4: "E_HIP",
            -5: "E_RCCL", -6: "E_NODEV", -7: "E_STATE"}
 
 
-def remap_flag(xcd_remap) -> int:
-    """None = library default (remap when the matrix fits the Infinity Cache)."""
+def remap_flag(xcd_remap, xcd_chunk: int = 0) -> int:
+    """None = library default (remap when the matrix fits the Infinity Cache);
+    xcd_chunk (a power of two) overrides: blocks per XCD turn, 1 = dispatch order."""
+    if xcd_chunk:
+        s = int(xcd_chunk)
+        if s < 1 or s & (s - 1):
+            raise ValueError("xcd_chunk must be a power of two >= 1")
+        return (s.bit_length()) << XCD_CHUNK_SHIFT
     if xcd_remap is None:
         return 0
     return FLAG_XCD_REMAP if xcd_remap else FLAG_NO_XCD_REMAP
+
+
+def groups_flag(groups: int) -> int:
+    if not groups:
+        return 0
+    g = int(groups)
+    if g not in (1, 2, 4, 8, 16):
+        raise ValueError("groups_per_wave must be one of 1, 2, 4, 8, 16")
+    return g.bit_length() << GROUPS_SHIFT
 
 
 def lanes_flag(lanes: int) -> int:
@@ -81,7 +98,7 @@ class Info(C.Structure):
     _fields_ = [("kernel", C.c_int32), ("lanes", C.c_int32), ("waves_per_block", C.c_int32),
                 ("num_gpus", C.c_int32), ("blocks", C.c_int64), ("alg_bytes", C.c_double),
                 ("flops", C.c_double), ("device_bytes", C.c_int64), ("chunk_u", C.c_int32),
-                ("n_split_rows", C.c_int32), ("xcd_remap", C.c_int32), ("reserved", C.c_int32),
+                ("n_split_rows", C.c_int32), ("xcd_remap", C.c_int32), ("groups_per_wave", C.c_int32),
                 ("x_entries", C.c_int64)]
 
 

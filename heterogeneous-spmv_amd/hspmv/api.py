@@ -243,12 +243,12 @@ class SpMV:
                  kernel: str = "auto", lanes: int = 0, nontemporal: bool = False,
                  device: Optional[int] = None, stream: Optional[int] = None,
                  xcd_remap: Optional[bool] = None, split_rows: bool = True, chunk_u: int = 0,
-                 prefetch: Optional[bool] = None):
+                 prefetch: Optional[bool] = None, xcd_chunk: int = 0, groups_per_wave: int = 0):
         self.A = A
         self.maps = maps
         self.dtype = A.val.dtype
         flags = _KERNELS[kernel] | lanes_flag(lanes) | (FLAG_NONTEMPORAL if nontemporal else 0)
-        flags |= remap_flag(xcd_remap)
+        flags |= remap_flag(xcd_remap, xcd_chunk) | _lib.groups_flag(groups_per_wave)
         flags |= (0 if split_rows else _lib.FLAG_NO_SPLIT)
         if chunk_u:
             if chunk_u not in (2, 3, 4, 6, 8, 16):
@@ -274,7 +274,8 @@ class SpMV:
                     *, device: int = 0, stream: Optional[int] = None, kernel: str = "auto",
                     lanes: int = 0, nontemporal: bool = False, xcd_remap: Optional[bool] = None,
                     split_rows: bool = True, chunk_u: int = 0,
-                    prefetch: Optional[bool] = None) -> "SpMV":
+                    prefetch: Optional[bool] = None, xcd_chunk: int = 0,
+                    groups_per_wave: int = 0) -> "SpMV":
         """Handle over caller-owned DEVICE arrays (HSPMV_FLAG_DEVICE_PTRS):
         csr_dev/maps_dev hold device pointers; A_meta supplies m, n, dtype."""
         self = cls.__new__(cls)
@@ -282,7 +283,8 @@ class SpMV:
         self.maps = None
         self.dtype = A_meta.val.dtype
         flags = (_KERNELS[kernel] | lanes_flag(lanes) | (FLAG_NONTEMPORAL if nontemporal else 0)
-                 | FLAG_DEVICE_PTRS | remap_flag(xcd_remap)
+                 | FLAG_DEVICE_PTRS | remap_flag(xcd_remap, xcd_chunk)
+                 | _lib.groups_flag(groups_per_wave)
                  | (0 if split_rows else _lib.FLAG_NO_SPLIT) | (chunk_u << _lib.U_SHIFT)
                  | (_lib.FLAG_PREFETCH if prefetch else 0))
         h = C.c_void_p()

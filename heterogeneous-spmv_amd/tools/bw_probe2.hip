@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #define CK(x)                                                                       \
@@ -91,7 +92,10 @@ float time_ms(F launch, int reps) {
   return t[0];
 }
 
-int main() {
+int main(int argc, char **argv) {
+  // optional: bw_probe2 SEG REMAP -- one configuration (for counter passes)
+  const int only_seg = argc > 1 ? atoi(argv[1]) : 0;
+  const int only_remap = argc > 2 ? atoi(argv[2]) : -1;
   // 50M nonzeros = 600 MB of col+val (C3-sized), far beyond the 256 MiB MALL
   const long nnz = 50L << 20;
   int *col;
@@ -103,9 +107,11 @@ int main() {
   CK(hipMemset(val, 0, nnz * 8));
   const double bytes = (double)nnz * 12;
   for (int seg : {640, 1728, 4096}) {
+    if (only_seg && seg != only_seg) continue;
     const long waves = (nnz + seg - 1) / seg;
     const unsigned grid = (unsigned)((waves + 3) / 4);
     for (int remap : {0, 1}) {
+      if (only_remap >= 0 && remap != only_remap) continue;
 #define RUN(U, W)                                                                              \
   bytes / time_ms([&] { hipLaunchKernelGGL((seg_read<U, W>), dim3(grid), dim3(256), 0, 0, col, \
                                            val, nnz, seg, remap, out); }, 10) * 1e-6

@@ -36,7 +36,7 @@ def main():
     if a.kernel != "csr3" and a.kernel != "auto":
         maps = None
     op = hspmv.SpMV(A, maps, kernel=a.kernel, chunk_u=a.u, lanes=a.lanes, prefetch=a.pf,
-                    nontemporal=a.nt, xcd_remap=not a.noxcd)
+                    nontemporal=a.nt, xcd_remap=False if a.noxcd else None)
     op.set_x(gen.rand_x(A.n, 42).astype(A.val.dtype))
     t = op.run(warmup=3, iters=a.iters)
     b = op.info["alg_bytes"]  # x counted as the distinct columns read

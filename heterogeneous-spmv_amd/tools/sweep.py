@@ -121,6 +121,28 @@ def variants(cfg, A, maps, full=False):
     return v
 
 
+def xcd_variants(A, maps):
+    d = A.nnz / A.m
+    m3 = maps if maps is not None else hspmv.build_csr3_maps(A, *hspmv.csr3_params(d, "mi355x"))
+    v = [("stream-auto", dict(kernel="stream"), None), ("csr3-auto", dict(kernel="csr3"), m3),
+         ("stream-xcdfull", dict(kernel="stream", xcd_remap=True), None),
+         ("csr3-xcdfull", dict(kernel="csr3", xcd_remap=True), m3)]
+    for s in (1, 2, 4, 8, 16, 32, 64, 128):
+        v.append((f"stream-xcd{s}", dict(kernel="stream", xcd_chunk=s), None))
+        v.append((f"csr3-xcd{s}", dict(kernel="csr3", xcd_chunk=s), m3))
+    return v
+
+
+def group_variants(A):
+    v = [("stream-auto", dict(kernel="stream"), None)]
+    for g in (1, 2, 4, 8, 16):
+        for u in (0, 2, 4, 6):
+            for pf in (False, True):
+                name = f"stream-g{g}" + (f"-u{u}" if u else "") + ("-pf" if pf else "")
+                v.append((name, dict(kernel="stream", groups_per_wave=g, chunk_u=u, prefetch=pf), None))
+    return v
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c2,c3,c4,c5")
@@ -128,6 +150,8 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--out", default="")
     ap.add_argument("--quick", action="store_true", help="only stream u4/u6 + csr3 auto")
+    ap.add_argument("--grid", default="main", choices=["main", "xcd", "groups"],
+                    help="xcd: the XCD chunk grid (blocks per XCD turn) at the auto chunk size")
     a = ap.parse_args()
     import oracle
     lines = []
@@ -140,7 +164,8 @@ def main():
         print(f"# {cfg}: {desc} m={A.m} nnz={A.nnz} built in {time.time() - t0:.1f}s",
               file=sys.stderr, flush=True)
         ops = []
-        vs = variants(cfg, A, maps)
+        vs = {"main": lambda: variants(cfg, A, maps), "xcd": lambda: xcd_variants(A, maps),
+              "groups": lambda: group_variants(A)}[a.grid]()
         if a.quick:
             vs = [v for v in vs if v[0] in ("stream-u4", "stream-u6", "stream-u8", "stream-auto",
                                           "stream-auto-noxcd", "csr3-auto", "csr3-mi355x-auto")]
@@ -149,6 +174,8 @@ def main():
         dev = DeviceMatrix(A, x)
         for name, kw, mp in vs:
             op = dev.spmv(mp, **kw)
+            dev.y.fill_(float("nan"))  # a row the kernel skips cannot pass
+            torch.cuda.synchronize()  # the fill runs on torch's stream, the SpMV on its own
             op.spmv()
             op.synchronize()
             y = dev.y.cpu().numpy()
@@ -173,7 +200,9 @@ def main():
                    "gbps_min": round(b / tmin * 1e-9, 1), "gbps_avg": round(b / tmed * 1e-9, 1),
                    "gflops_min": round(2 * A.nnz / tmin * 1e-9, 1), "frac_peak": round(b / tmin * 1e-9 / PEAK, 4),
                    "chunk_u": op.info["chunk_u"], "waves_per_block": op.info["waves_per_block"],
-                   "n_split_rows": op.info["n_split_rows"], "desc": desc}
+                   "n_split_rows": op.info["n_split_rows"], "xcd_chunk": op.info["xcd_remap"],
+                   "groups": op.info["groups_per_wave"],
+                   "desc": desc}
             lines.append(rec)
             print(json.dumps(rec), flush=True)
             op.close()

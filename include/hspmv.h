@@ -114,8 +114,8 @@ typedef struct {
   int64_t device_bytes; /* device memory held by the handle (all GPUs)     */
   int32_t chunk_u;    /* STREAM/CSR3 elements per lane per LDS chunk        */
   int32_t n_split_rows; /* rows summed by the split-row kernels (GPU 0)     */
-  int32_t xcd_remap;  /* 1 = XCD-contiguous block order                    */
-  int32_t reserved;
+  int32_t xcd_remap;  /* blocks per XCD turn (1 = dispatch order)          */
+  int32_t groups_per_wave; /* STREAM: 64-row groups one wave walks        */
   int64_t x_entries;  /* distinct columns referenced = x entries one SpMV
                          must read (summed over GPUs); alg_bytes uses it    */
 } hspmv_info;
@@ -151,6 +151,15 @@ typedef struct hspmv_handle hspmv_handle;
                                           col/val loads one chunk ahead   */
 #define HSPMV_FLAG_XCD_REMAP (1u << 22) /* force the XCD-contiguous block
                                            order whatever the size         */
+/* Explicit XCD chunk: HSPMV_XCD_CHUNK(s), s a power of two >= 1: each XCD
+ * takes s consecutive blocks in turn (1 = dispatch order).  Overrides the
+ * two flags above; 0 = automatic. */
+#define HSPMV_XCD_CHUNK_SHIFT 24
+#define HSPMV_XCD_CHUNK(s) ((unsigned)(__builtin_ctz((unsigned)(s)) + 1) << HSPMV_XCD_CHUNK_SHIFT)
+/* STREAM: 64-row groups per wave, HSPMV_GROUPS(g), g in {1,2,4,8,16}; the
+ * next group's row pointers are loaded while this one streams.  0 = auto. */
+#define HSPMV_GROUPS_SHIFT 29
+#define HSPMV_GROUPS(g) ((unsigned)(__builtin_ctz((unsigned)(g)) + 1) << HSPMV_GROUPS_SHIFT)
 
 /* ---------------------------------------------------------------- handle */
 /* Upload A (and optional CSR-3 maps) to num_gpus devices (0 = all visible).

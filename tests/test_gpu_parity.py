@@ -273,10 +273,21 @@ def test_chunk_u_and_remap_variants():
         for u in (2, 3, 4, 6, 8, 16):
             for remap, pf in ((True, False), (False, True), (True, True)):
                 y, info = gpu_spmv(A, x, kernel="stream", chunk_u=u, xcd_remap=remap, prefetch=pf)
-                assert info["chunk_u"] == u and info["xcd_remap"] == int(remap)
+                assert info["chunk_u"] == u and (info["xcd_remap"] > 1) == remap
                 ys.append(y)
                 y3, _ = gpu_spmv(A, x, maps, chunk_u=u, xcd_remap=remap, prefetch=pf)
                 ys.append(y3)
+        for g in (2, 4, 16):  # several 64-row groups per wave, rp prefetched
+            for pf in (False, True):
+                y, info = gpu_spmv(A, x, kernel="stream", groups_per_wave=g, prefetch=pf)
+                assert info["groups_per_wave"] == g
+                ys.append(y)
+        for xc in (2, 4, 16):  # chunked XCD orders (tail blocks keep their index)
+            y, info = gpu_spmv(A, x, kernel="stream", xcd_chunk=xc)
+            assert info["xcd_remap"] == xc
+            ys.append(y)
+            y3, _ = gpu_spmv(A, x, maps, xcd_chunk=xc)
+            ys.append(y3)
         ok = short_rows(A)
         y64 = check_fp64(A, x, ys[0], exact_rows=ok)
         absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
