@@ -12,8 +12,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "hspmv_common.h"
@@ -48,6 +50,9 @@ struct Shard {
   double mean_rows_per_ssr = 0.0;
   // owned device memory
   int32_t *d_rp = nullptr, *d_ci = nullptr, *d_outer = nullptr, *d_inner = nullptr;
+  uint16_t *d_c16 = nullptr;  // 16-bit column offsets (owned even for borrowed A)
+  int32_t *d_cbase = nullptr;
+  uint64_t *d_cplanes = nullptr;
   void *d_val = nullptr;
   void *d_x = nullptr;     // own x (n entries)
   void *d_y = nullptr;     // own y (m_shard entries) -- or a slice of d_yfull
@@ -57,6 +62,7 @@ struct Shard {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int64_t bytes = 0;
   int64_t x_entries = 0;   // distinct columns of this shard
+  double c16_saved = 0.0;  // bytes per SpMV the 16-bit column offsets save
   // planner tables (owned): CSR-3 wave tasks and split-row chunks
   DevPlan dp;
   int32_t *d_task = nullptr, *d_long_row = nullptr, *d_long_cstart = nullptr,
@@ -110,6 +116,9 @@ void free_shard(Shard &s, bool borrowed) {
     (void)hipFree(s.d_outer);
     (void)hipFree(s.d_inner);
   }
+  (void)hipFree(s.d_c16);
+  (void)hipFree(s.d_cbase);
+  (void)hipFree(s.d_cplanes);
   (void)hipFree(s.d_task);
   (void)hipFree(s.d_long_row);
   (void)hipFree(s.d_long_cstart);
@@ -133,9 +142,90 @@ int64_t count_distinct_cols(const int32_t *col, int64_t nnz, int64_t n) {
   return c;
 }
 
+// 16-bit column offsets: per block of 2^kC16Shift nonzeros, base = the
+// block's smallest column and col - base split into its low 16 bits (off16)
+// and k high bits stored as k bit-planes of 64-bit words (bit k&63 of word
+// k>>6), k = the fewest that cover every block's column span.  Used when
+// k <= kMaxC16Planes and the shard streams from HBM.  One-process A/B
+// runs (profiles/r01_ab_col16.jsonl): C4 (k = 0) -10 %, C3 (k = 1) -5 %;
+// C5 (k = 5) +9 % and the Infinity-Cache-resident C2 +4 % slower, where the
+// extra scalar loads and selects outweigh the bytes saved.
+constexpr int kMaxC16Planes = 1;
+constexpr int kMaxC16PlanesForced = 8;  // 3 index bytes: still fewer than 4
+constexpr double kMallResident = 192.0 * 1024 * 1024;  // same bound as the XCD order
+
+int build_col16(Shard &s, const int32_t *col, int64_t nnz, int64_t m, int64_t n, int dtype,
+                unsigned flags, bool *used) {
+  *used = false;
+  if ((flags & HSPMV_FLAG_NO_COL16) || nnz == 0) return HSPMV_OK;
+  const bool forced = (flags & HSPMV_FLAG_COL16) != 0;
+  const double sv = (double)dtype_size(dtype);
+  if (!forced && (double)nnz * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv <= kMallResident)
+    return HSPMV_OK;
+  const int64_t B = int64_t(1) << kC16Shift;
+  const int64_t nb = (nnz + B - 1) / B;
+  std::vector<int32_t> base((size_t)nb + 1, 0);  // +1: kernels load bases in pairs
+  std::vector<int32_t> span((size_t)nb, 0);
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, nb / 4096));
+  auto par = [&](auto &&body) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back([&, t]() { body(nb * t / nt, nb * (t + 1) / nt); });
+    for (auto &x : th) x.join();
+  };
+  par([&](int64_t b0, int64_t b1) {
+    for (int64_t b = b0; b < b1; ++b) {
+      const int64_t k0 = b * B, k1 = std::min(nnz, k0 + B);
+      int32_t lo = col[k0], hi = col[k0];
+      for (int64_t k = k0 + 1; k < k1; ++k) {
+        lo = std::min(lo, col[k]);
+        hi = std::max(hi, col[k]);
+      }
+      base[(size_t)b] = lo;
+      span[(size_t)b] = hi - lo;
+    }
+  });
+  int32_t maxspan = 0;
+  for (int32_t v : span) maxspan = std::max(maxspan, v);
+  int bits = 0;
+  while (bits < 31 && (int64_t(1) << bits) <= maxspan) ++bits;
+  const int planes = std::max(0, bits - 16);
+  if (planes > (forced ? kMaxC16PlanesForced : kMaxC16Planes)) return HSPMV_OK;
+  const int64_t nw = (nnz + 63) / 64 + 1;  // +1: kernels load words in pairs
+  std::vector<uint16_t> off((size_t)nnz);
+  std::vector<uint64_t> pl((size_t)(planes * nw), 0);
+  par([&](int64_t b0, int64_t b1) {
+    // blocks are 4 words wide, so threads never share a plane word
+    for (int64_t b = b0; b < b1; ++b) {
+      const int64_t k0 = b * B, k1 = std::min(nnz, k0 + B);
+      for (int64_t k = k0; k < k1; ++k) {
+        const uint32_t d = (uint32_t)(col[k] - base[(size_t)b]);
+        off[(size_t)k] = (uint16_t)d;
+        for (int p = 0; p < planes; ++p)
+          pl[(size_t)(p * nw + (k >> 6))] |= (uint64_t)((d >> (16 + p)) & 1u) << (k & 63);
+      }
+    }
+  });
+  int rc;
+  if ((rc = dev_alloc(&s.d_c16, 2 * (size_t)nnz, &s.bytes))) return rc;
+  if ((rc = dev_alloc(&s.d_cbase, 4 * (size_t)(nb + 1), &s.bytes))) return rc;
+  HIP_TRY(hipMemcpy(s.d_c16, off.data(), 2 * (size_t)nnz, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s.d_cbase, base.data(), 4 * (size_t)(nb + 1), hipMemcpyHostToDevice));
+  if (planes) {
+    if ((rc = dev_alloc(&s.d_cplanes, 8 * pl.size(), &s.bytes))) return rc;
+    HIP_TRY(hipMemcpy(s.d_cplanes, pl.data(), 8 * pl.size(), hipMemcpyHostToDevice));
+  }
+  s.A.col16 = s.d_c16;
+  s.A.cbase = s.d_cbase;
+  s.A.cplanes = s.d_cplanes;
+  s.A.n_cplanes = planes;
+  s.A.cplane_words = (int32_t)nw;
+  *used = true;
+  return HSPMV_OK;
+}
+
 // Uploads rows [r0, r1) of A (and the matching slice of the maps) to shard s.
 int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_t r0, int64_t r1,
-                 int64_t ssr0, int64_t ssr1, int64_t y_rows_alloc) {
+                 int64_t ssr0, int64_t ssr1, int64_t y_rows_alloc, unsigned flags) {
   const size_t sv = dtype_size(A->dtype);
   const int64_t m = r1 - r0;
   const int64_t k0 = A->row_ptr[r0], k1 = A->row_ptr[r1];
@@ -166,6 +256,8 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
   s.A.row_ptr = s.d_rp;
   s.A.col_idx = s.d_ci;
   s.A.val = s.d_val;
+  bool c16 = false;
+  if ((rc = build_col16(s, A->col_idx + k0, nnz, m, A->n, A->dtype, flags, &c16))) return rc;
   if (mp && mp->n_ssr > 0) {
     const int64_t nssr = ssr1 - ssr0;
     const int64_t sr0 = mp->outer[ssr0], sr1 = mp->outer[ssr1];
@@ -198,11 +290,13 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
   const std::vector<int32_t> &rp = s.h_rp;
   const int64_t m = s.A.m;
   s.dp = DevPlan();
+  int64_t long_nnz = 0;
   if (s.plan.kernel != kVector && !(flags & HSPMV_FLAG_NO_SPLIT)) {
     std::vector<int32_t> lrow, lcs(1, 0), ck;
     for (int64_t r = 0; r < m; ++r) {
       const int32_t b = rp[r], e = rp[r + 1];
       if (e - b <= kLongRow) continue;
+      long_nnz += e - b;
       lrow.push_back((int32_t)r);
       for (int32_t k = b; k < e; k += kLongChunk) {
         ck.push_back(k);
@@ -228,6 +322,17 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
       s.dp.chunk_k = s.d_chunk_k;
       s.dp.partials = s.d_partials;
     }
+  }
+  if (s.plan.kernel == kVector) {
+    s.A.col16 = nullptr;  // the vector kernel reads 32-bit columns
+    s.A.cbase = nullptr;
+    s.A.cplanes = nullptr;
+    s.A.n_cplanes = 0;
+  }
+  if (s.A.col16) {
+    const int64_t nb = (s.A.nnz + (int64_t(1) << kC16Shift) - 1) >> kC16Shift;
+    s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)nb -
+                  (double)s.A.n_cplanes * (double)(s.A.nnz - long_nnz) / 8.0;
   }
   if (s.plan.kernel == kCsr3) {
     const std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
@@ -320,7 +425,7 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
     if ((rc = validate_host_csr(A, true))) return rc;
     if ((rc = validate_host_maps(maps, A->m))) return rc;
     if (maps && maps->n_ssr > 0) { h->n_ssr = maps->n_ssr; h->n_sr = maps->n_sr; }
-    if ((rc = upload_shard(s, A, maps, 0, A->m, 0, maps ? maps->n_ssr : 0, A->m))) {
+    if ((rc = upload_shard(s, A, maps, 0, A->m, 0, maps ? maps->n_ssr : 0, A->m, flags))) {
       free_shard(s, false);
       return rc;
     }
@@ -347,6 +452,8 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
       for (int32_t c : cols)
         if (c < 0 || c >= A->n) return set_error(HSPMV_E_INVALID, "device col_idx %d out of [0, %lld)", c, (long long)A->n);
       s.x_entries = count_distinct_cols(cols.data(), A->nnz, A->n);
+      bool c16 = false;
+      if ((rc = build_col16(s, cols.data(), A->nnz, A->m, A->n, A->dtype, flags, &c16))) return rc;
     }
     if (maps && maps->n_ssr > 0) {
       std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
@@ -418,7 +525,8 @@ int hspmv_create(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *m
   for (int p = 0; p < num_gpus; ++p) {
     Shard &s = h->shards[p];
     s.device = p;
-    if ((rc = upload_shard(s, A, maps, splits[p], splits[p + 1], ssr_split[p], ssr_split[p + 1], 0))) {
+    if ((rc = upload_shard(s, A, maps, splits[p], splits[p + 1], ssr_split[p], ssr_split[p + 1], 0,
+                           flags))) {
       cleanup();
       return rc;
     }
@@ -656,6 +764,9 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->n_split_rows = s.dp.n_long;
   out->xcd_remap = s.plan.xcd_chunk;
   out->groups_per_wave = s.plan.kernel == kStream ? s.plan.groups : 1;
+  out->format_bytes = out->alg_bytes;
+  for (auto &sh : h->shards) out->format_bytes -= sh.c16_saved;
+  out->col16 = s.A.col16 ? 1 + s.A.n_cplanes : 0;
   return HSPMV_OK;
 }
 

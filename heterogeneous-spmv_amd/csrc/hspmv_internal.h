@@ -17,7 +17,15 @@ struct DevCSR {
   int32_t n_ssr = 0, n_sr = 0;          // CSR-3 maps (0 = none)
   const int32_t *outer = nullptr;
   const int32_t *inner = nullptr;
+  // 16-bit column offsets (row kernels): col[k] = cbase[k >> kC16Shift] + col16[k]
+  // plus bit 16+p of (col - base) in plane p: bit k&63 of cplanes[p*cplane_words + k/64]
+  const uint16_t *col16 = nullptr;
+  const int32_t *cbase = nullptr;
+  const uint64_t *cplanes = nullptr;
+  int32_t n_cplanes = 0, cplane_words = 0;
 };
+
+constexpr int kC16Shift = 8;  // 256 nonzeros per column-base block
 
 enum Kernel : int { kAuto = 0, kVector = 1, kStream = 2, kCsr3 = 3 };
 

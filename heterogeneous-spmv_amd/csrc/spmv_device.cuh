@@ -111,6 +111,16 @@ __device__ __forceinline__ const gchar *uniform_ptr(const T *p) {
   return (const gchar *)(((uint64_t)hi << 32) | lo);
 }
 
+// Scalar (s_load) read of 8 bytes at p + byte_off; p and byte_off must be
+// wave-uniform.
+__device__ __forceinline__ int64_t sload_i64(const void *p, uint64_t byte_off) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p) + byte_off;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  typedef __attribute__((address_space(4))) const int64_t ci64;
+  return *(ci64 *)(((uint64_t)hi << 32) | lo);
+}
+
 // Ordered sum of lds[lo..hi) into acc, left to right: the LDS reads are
 // issued 4 at a time (one LDS latency per 4 nonzeros instead of per nonzero)
 // but the additions stay in sequence, so the rounding is omp_spmv's.
@@ -146,10 +156,14 @@ __device__ __forceinline__ void group_bounds(const int32_t *__restrict__ rp, int
 // sums.  PF (software pipelining): the next chunk's stage A is issued
 // between this chunk's stage B and C, so its latency overlaps the gather and
 // the sums.
-template <typename T, bool NT, int U, bool PF>
+template <typename T, bool NT, int U, bool PF, bool C16>
 __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, int32_t end,
                                           int32_t long_t,
                                           const int32_t *__restrict__ ci,
+                                          const uint16_t *__restrict__ c16,
+                                          const int32_t *__restrict__ cbase,
+                                          const uint64_t *__restrict__ cplanes,
+                                          int32_t n_planes, int32_t plane_words,
                                           const T *__restrict__ val,
                                           const T *__restrict__ x,
                                           T *__restrict__ y, T *lds, int lane,
@@ -177,7 +191,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
       const bool mine = serial && row >= a && row < b;
       int32_t col[U];
       T v[U];
-      const gchar *cb = uniform_ptr(ci + kb);
+      const gchar *cb = C16 ? uniform_ptr(c16 + kb) : uniform_ptr(ci + kb);
       const gchar *vb = uniform_ptr(val + kb);
       // (A raw-buffer form -- SGPR descriptors bounded to the run, no
       // clamp VALU -- measured 0-2.5 % slower in one-process A/B runs,
@@ -187,7 +201,30 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         for (int u = 0; u < U; ++u) {
           // clamp instead of branching: every load issues back to back
           const uint32_t j = (uint32_t)(c0 + min(u * kWave + lane, last));
-          col[u] = ld_off<NT, int32_t>(cb, j * 4u);
+          if constexpr (C16) {
+            // col = base of the nonzero's 256-block + 16-bit offset.  The 64
+            // lanes of a slice lie in at most two consecutive blocks: one
+            // scalar load brings both bases (s_load, no vector memory op)
+            const uint32_t e0 = (uint32_t)kb + (uint32_t)(c0 + min(u * kWave, last));
+            const uint32_t ja = (uint32_t)kb + j;
+            const uint32_t b0 = __builtin_amdgcn_readfirstlane(e0 >> kC16Shift);
+            const int64_t bp = sload_i64(cbase, (uint64_t)b0 * 4u);
+            const int32_t base = ((ja >> kC16Shift) == b0) ? (int32_t)bp : (int32_t)(bp >> 32);
+            int32_t high = 0;
+            if (n_planes > 0) {  // wave-uniform; the two words a slice spans, by s_load
+              const uint32_t w0 = __builtin_amdgcn_readfirstlane(e0 >> 6);
+              const bool first = (ja >> 6) == w0;
+              for (int p = 0; p < n_planes; ++p) {
+                const uint64_t at = ((uint64_t)p * (uint64_t)plane_words + w0) * 8u;
+                const uint64_t m0 = (uint64_t)sload_i64(cplanes, at);
+                const uint64_t m1 = (uint64_t)sload_i64(cplanes, at + 8u);
+                high |= (int32_t)(((first ? m0 : m1) >> (ja & 63u)) & 1u) << p;
+              }
+            }
+            col[u] = base + (int32_t)ld_off<NT, uint16_t>(cb, j * 2u) + (high << 16);
+          } else {
+            col[u] = ld_off<NT, int32_t>(cb, j * 4u);
+          }
           v[u] = ld_off<NT, T>(vb, j * (uint32_t)sizeof(T));
         }
       };
@@ -258,11 +295,13 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
 // STREAM: wave w walks `groups` consecutive 64-row groups starting at row
 // w * groups * 64, loading the next group's row pointers before streaming
 // the current one.
-template <typename T, bool NT, int U, bool PF>
+template <typename T, bool NT, int U, bool PF, bool C16>
 __global__ __launch_bounds__(256) void hspmv_csr_stream(
     int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups,
-    const int32_t *__restrict__ rp, const int32_t *__restrict__ ci, const T *__restrict__ val,
-    const T *__restrict__ x, T *__restrict__ y) {
+    const int32_t *__restrict__ rp, const int32_t *__restrict__ ci,
+    const uint16_t *__restrict__ c16, const int32_t *__restrict__ cbase,
+    const uint64_t *__restrict__ cplanes, int32_t n_planes, int32_t plane_words,
+    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[4 * kWave * U];
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
@@ -291,7 +330,8 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
     const int32_t g1 = (int32_t)min<int64_t>(g0 + kWave, gend);
     int32_t nbeg = 0, nend = 0;
     if (g1 < gend) group_bounds(rp, g1, (int32_t)min<int64_t>(g1 + kWave, gend), lane, nbeg, nend);
-    wave_rows<T, NT, U, PF>((int32_t)g0, g1, beg, end, long_t, ci, val, x, y, my, lane, ts);
+    wave_rows<T, NT, U, PF, C16>((int32_t)g0, g1, beg, end, long_t, ci, c16, cbase, cplanes,
+                                 n_planes, plane_words, val, x, y, my, lane, ts);
     ts = nullptr;  // trace the first group only
     if (g1 >= gend) break;
     g0 = g1;
@@ -300,11 +340,13 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
   }
 }
 
-template <typename T, bool NT, int U, bool PF, int W>
+template <typename T, bool NT, int U, bool PF, bool C16, int W>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, const int32_t *__restrict__ task_start,
-    const int32_t *__restrict__ rp, const int32_t *__restrict__ ci, const T *__restrict__ val,
-    const T *__restrict__ x, T *__restrict__ y) {
+    const int32_t *__restrict__ rp, const int32_t *__restrict__ ci,
+    const uint16_t *__restrict__ c16, const int32_t *__restrict__ cbase,
+    const uint64_t *__restrict__ cplanes, int32_t n_planes, int32_t plane_words,
+    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[W * kWave * U];
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
@@ -321,7 +363,8 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     const int32_t g1 = min(g0 + kWave, r1);
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
-    wave_rows<T, NT, U, PF>(g0, g1, beg, end, long_t, ci, val, x, y, my, lane);
+    wave_rows<T, NT, U, PF, C16>(g0, g1, beg, end, long_t, ci, c16, cbase, cplanes, n_planes,
+                                 plane_words, val, x, y, my, lane);
     beg = nbeg;
     end = nend;
   }
@@ -329,19 +372,22 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
 
 // ------------------------------------------------------------------ launchers
 
-template <typename T, bool NT, int U, bool PF>
+template <typename T, bool NT, int U, bool PF, bool C16>
 void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x, T *y,
                    hipStream_t st) {
   const T *val = static_cast<const T *>(A.val);
   if (p.kernel == kStream) {
-    hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF>), dim3((unsigned)p.blocks), dim3(256), 0,
-                       st, A.m, dp.long_t, (uint32_t)p.xcd_chunk, (int32_t)p.groups, A.row_ptr, A.col_idx, val, x, y);
+    hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16>), dim3((unsigned)p.blocks), dim3(256),
+                       0, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk, (int32_t)p.groups, A.row_ptr,
+                       A.col_idx, A.col16, A.cbase, A.cplanes, A.n_cplanes, A.cplane_words, val,
+                       x, y);
     return;
   }
-#define HSPMV_CSR3(W)                                                                        \
-  hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, W>), dim3((unsigned)p.blocks), dim3(W * 64), 0, \
-                     st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk, dp.task_start,                \
-                     A.row_ptr, A.col_idx, val, x, y)
+#define HSPMV_CSR3(W)                                                                     \
+  hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C16, W>), dim3((unsigned)p.blocks),        \
+                     dim3(W * 64), 0, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,   \
+                     dp.task_start, A.row_ptr, A.col_idx, A.col16, A.cbase, A.cplanes,     \
+                     A.n_cplanes, A.cplane_words, val, x, y)
   switch (p.waves_per_block) {
     case 1: HSPMV_CSR3(1); break;
     case 2: HSPMV_CSR3(2); break;
@@ -351,29 +397,36 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
 #undef HSPMV_CSR3
 }
 
-template <typename T, bool NT, bool PF>
+template <typename T, bool NT, bool PF, bool C16>
 hipError_t launch_rows_pf(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x,
                           T *y, hipStream_t st) {
   switch (p.u) {
-    case 2: launch_rows_u<T, NT, 2, PF>(A, dp, p, x, y, st); break;
-    case 3: launch_rows_u<T, NT, 3, PF>(A, dp, p, x, y, st); break;
-    case 4: launch_rows_u<T, NT, 4, PF>(A, dp, p, x, y, st); break;
-    case 6: launch_rows_u<T, NT, 6, PF>(A, dp, p, x, y, st); break;
-    case 8: launch_rows_u<T, NT, 8, PF>(A, dp, p, x, y, st); break;
-    case 16: launch_rows_u<T, NT, 16, PF>(A, dp, p, x, y, st); break;
+    case 2: launch_rows_u<T, NT, 2, PF, C16>(A, dp, p, x, y, st); break;
+    case 3: launch_rows_u<T, NT, 3, PF, C16>(A, dp, p, x, y, st); break;
+    case 4: launch_rows_u<T, NT, 4, PF, C16>(A, dp, p, x, y, st); break;
+    case 6: launch_rows_u<T, NT, 6, PF, C16>(A, dp, p, x, y, st); break;
+    case 8: launch_rows_u<T, NT, 8, PF, C16>(A, dp, p, x, y, st); break;
+    case 16: launch_rows_u<T, NT, 16, PF, C16>(A, dp, p, x, y, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
+template <typename T, bool C16>
+hipError_t launch_rows_c(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x,
+                         T *y, hipStream_t st) {
+  if (p.nontemporal)
+    return p.prefetch ? launch_rows_pf<T, true, true, C16>(A, dp, p, x, y, st)
+                      : launch_rows_pf<T, true, false, C16>(A, dp, p, x, y, st);
+  return p.prefetch ? launch_rows_pf<T, false, true, C16>(A, dp, p, x, y, st)
+                    : launch_rows_pf<T, false, false, C16>(A, dp, p, x, y, st);
+}
+
 template <typename T>
 hipError_t launch_rows(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x, T *y,
                        hipStream_t st) {
-  if (p.nontemporal)
-    return p.prefetch ? launch_rows_pf<T, true, true>(A, dp, p, x, y, st)
-                      : launch_rows_pf<T, true, false>(A, dp, p, x, y, st);
-  return p.prefetch ? launch_rows_pf<T, false, true>(A, dp, p, x, y, st)
-                    : launch_rows_pf<T, false, false>(A, dp, p, x, y, st);
+  return A.col16 ? launch_rows_c<T, true>(A, dp, p, x, y, st)
+                 : launch_rows_c<T, false>(A, dp, p, x, y, st);
 }
 
 }  // namespace dev

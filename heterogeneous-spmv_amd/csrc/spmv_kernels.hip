@@ -189,6 +189,7 @@ int pick_u(double nnz_per_pass, int dtype) {
   if (nnz_per_pass <= 192.0) return 3;
   if (nnz_per_pass <= 256.0) return 4;
   if (nnz_per_pass <= 384.0) return 6;
+  if (dtype == 1 && nnz_per_pass <= 768.0) return 6;  // two chunks (C4: -1.5 %, r01_ab_col16)
   return dtype == 1 ? 4 : 8;
 }
 

@@ -19,6 +19,7 @@ F32, F64 = 0, 1
 
 KERNEL_AUTO, KERNEL_VECTOR, KERNEL_STREAM, KERNEL_CSR3 = 0, 1, 2, 3
 LANES_SHIFT = 4
+FLAG_NO_COL16 = 1 << 11
 FLAG_NONTEMPORAL = 1 << 12
 FLAG_DEVICE_PTRS = 1 << 13
 FLAG_NO_XCD_REMAP = 1 << 14
@@ -26,6 +27,7 @@ FLAG_NO_SPLIT = 1 << 15
 U_SHIFT = 16
 FLAG_PREFETCH = 1 << 21
 FLAG_XCD_REMAP = 1 << 22
+FLAG_COL16 = 1 << 23
 XCD_CHUNK_SHIFT = 24
 GROUPS_SHIFT = 29
 
@@ -44,6 +46,14 @@ def remap_flag(xcd_remap, xcd_chunk: int = 0) -> int:
     if xcd_remap is None:
         return 0
     return FLAG_XCD_REMAP if xcd_remap else FLAG_NO_XCD_REMAP
+
+
+def col16_flag(col16) -> int:
+    """None = library default (HBM-resident matrices, <= 1 high-bit plane);
+    True forces 16-bit column offsets (<= 8 planes); False keeps 32-bit."""
+    if col16 is None:
+        return 0
+    return FLAG_COL16 if col16 else FLAG_NO_COL16
 
 
 def groups_flag(groups: int) -> int:
@@ -99,7 +109,8 @@ class Info(C.Structure):
                 ("num_gpus", C.c_int32), ("blocks", C.c_int64), ("alg_bytes", C.c_double),
                 ("flops", C.c_double), ("device_bytes", C.c_int64), ("chunk_u", C.c_int32),
                 ("n_split_rows", C.c_int32), ("xcd_remap", C.c_int32), ("groups_per_wave", C.c_int32),
-                ("x_entries", C.c_int64)]
+                ("x_entries", C.c_int64), ("format_bytes", C.c_double), ("col16", C.c_int32),
+                ("pad_", C.c_int32)]
 
 
 _P = C.c_void_p

@@ -243,12 +243,14 @@ class SpMV:
                  kernel: str = "auto", lanes: int = 0, nontemporal: bool = False,
                  device: Optional[int] = None, stream: Optional[int] = None,
                  xcd_remap: Optional[bool] = None, split_rows: bool = True, chunk_u: int = 0,
-                 prefetch: Optional[bool] = None, xcd_chunk: int = 0, groups_per_wave: int = 0):
+                 prefetch: Optional[bool] = None, xcd_chunk: int = 0, groups_per_wave: int = 0,
+                 col16: Optional[bool] = None):
         self.A = A
         self.maps = maps
         self.dtype = A.val.dtype
         flags = _KERNELS[kernel] | lanes_flag(lanes) | (FLAG_NONTEMPORAL if nontemporal else 0)
         flags |= remap_flag(xcd_remap, xcd_chunk) | _lib.groups_flag(groups_per_wave)
+        flags |= _lib.col16_flag(col16)
         flags |= (0 if split_rows else _lib.FLAG_NO_SPLIT)
         if chunk_u:
             if chunk_u not in (2, 3, 4, 6, 8, 16):
@@ -275,7 +277,7 @@ class SpMV:
                     lanes: int = 0, nontemporal: bool = False, xcd_remap: Optional[bool] = None,
                     split_rows: bool = True, chunk_u: int = 0,
                     prefetch: Optional[bool] = None, xcd_chunk: int = 0,
-                    groups_per_wave: int = 0) -> "SpMV":
+                    groups_per_wave: int = 0, col16: Optional[bool] = None) -> "SpMV":
         """Handle over caller-owned DEVICE arrays (HSPMV_FLAG_DEVICE_PTRS):
         csr_dev/maps_dev hold device pointers; A_meta supplies m, n, dtype."""
         self = cls.__new__(cls)
@@ -284,7 +286,7 @@ class SpMV:
         self.dtype = A_meta.val.dtype
         flags = (_KERNELS[kernel] | lanes_flag(lanes) | (FLAG_NONTEMPORAL if nontemporal else 0)
                  | FLAG_DEVICE_PTRS | remap_flag(xcd_remap, xcd_chunk)
-                 | _lib.groups_flag(groups_per_wave)
+                 | _lib.groups_flag(groups_per_wave) | _lib.col16_flag(col16)
                  | (0 if split_rows else _lib.FLAG_NO_SPLIT) | (chunk_u << _lib.U_SHIFT)
                  | (_lib.FLAG_PREFETCH if prefetch else 0))
         h = C.c_void_p()

@@ -45,18 +45,22 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    libs = [load(p) for p in a.libs.split(",")]
-    names = [Path(p).parent.name + "/" + Path(p).name for p in a.libs.split(",")]
+    # each entry: path[@flags] (flags ORed with --flags for that handle)
+    entries = [(e.split("@")[0], int(e.split("@")[1]) if "@" in e else 0) for e in a.libs.split(",")]
+    cache = {}
+    libs = [cache.setdefault(p, load(p)) for p, _ in entries]
+    extra = [f for _, f in entries]
+    names = [Path(p).parent.name + "/" + Path(p).name + (f"@{f}" if f else "") for p, f in entries]
     out = []
     for cfg in a.configs.split(","):
         A, maps, desc = build(cfg)
         x = gen.rand_x(A.n, 42).astype(A.val.dtype)
         cs, ms = A.c_struct(), (maps.c_struct() if maps is not None and a.kernel != "stream" else None)
         hs = []
-        for L in libs:
+        for L, fx in zip(libs, extra):
             h = C.c_void_p()
             rc = L.hspmv_create_on_device(C.byref(h), C.byref(cs), C.byref(ms) if ms else None, 0,
-                                          None, _KERNELS[a.kernel] | a.flags)
+                                          None, _KERNELS[a.kernel] | a.flags | fx)
             assert rc == 0, L.hspmv_last_error()
             assert L.hspmv_set_x(h, x.ctypes.data) == 0
             hs.append(h)
@@ -79,6 +83,7 @@ def main():
                    "y_equal_to_first": same[i]}
             out.append(rec)
             print(json.dumps(rec), flush=True)
+        for L, h in zip(libs, hs):
             L.hspmv_destroy(h)
     if a.out:
         Path(a.out).write_text("".join(json.dumps(r) + "\n" for r in out))

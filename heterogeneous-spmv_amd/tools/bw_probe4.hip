@@ -1,0 +1,124 @@
+// bw_probe4.hip -- calibration microbenchmark (not product code): cache
+// policy of the col/val stream loads and of the y stores (gfx950 cpol bits
+// in the raw-buffer aux operand: sc0 = 1, nt = 2, sc1 = 16) against the
+// cost of the y writes (bw_probe3: +21 % time for 6 % more bytes), in the
+// repeated-launch state the SpMV runs in.  Shape = bw_probe3 "+y" at
+// 10 nnz/row: one wave per 64 rows, U = 4 chunks, 64 y values per wave.
+//
+//   hipcc -O3 --offload-arch=gfx950 bw_probe4.hip -o bw_probe4 && ./bw_probe4
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#define CK(x)                                                                       \
+  do {                                                                              \
+    hipError_t e = (x);                                                             \
+    if (e != hipSuccess) {                                                          \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                        \
+      return 1;                                                                     \
+    }                                                                               \
+  } while (0)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, long bytes) {
+  const unsigned long v = (unsigned long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  const int n = (int)std::min(bytes, 0x7FFFFFFFL);
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((unsigned long)hi << 32) | lo), 0, n, 0x00020000);
+}
+
+template <int LAUX, int SAUX, bool STORE>
+__global__ __launch_bounds__(256) void probe(const int *__restrict__ col,
+                                             const double *__restrict__ val,
+                                             double *__restrict__ y, long nnz, double *out) {
+  constexpr int U = 4, PER_ROW = 10;
+  const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const long s0 = w * 64 * PER_ROW;
+  if (s0 >= nnz) return;
+  const auto rc = rsrc(col + s0, (nnz - s0) * 4);
+  const auto rv = rsrc(val + s0, (nnz - s0) * 8);
+  double s = 0.0;
+  for (int c = 0; c < 64 * PER_ROW; c += 64 * U) {
+    int cv[U];
+    double vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      cv[u] = __builtin_amdgcn_raw_buffer_load_b32(rc, (lane + u * 64) * 4, c * 4, LAUX);
+      const auto t = __builtin_amdgcn_raw_buffer_load_b64(rv, (lane + u * 64) * 8, c * 8, LAUX);
+      __builtin_memcpy(&vv[u], &t, 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += vv[u] * (double)cv[u];
+  }
+  if constexpr (STORE) {
+    const auto ry = rsrc(y + w * 64, 64 * 8);
+    unsigned long bits;
+    __builtin_memcpy(&bits, &s, 8);
+    __builtin_amdgcn_raw_buffer_store_b64(*(decltype(__builtin_amdgcn_raw_buffer_load_b64(ry, 0, 0, 0)) *)&bits,
+                                          ry, lane * 8, 0, SAUX);
+  } else {
+    if (s == 12345.678) out[0] = s;
+  }
+}
+
+template <typename F>
+float time_ms(F launch, int reps) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  std::vector<float> t;
+  for (int r = 0; r < reps + 3; ++r) {
+    (void)hipEventRecord(a);
+    launch();
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    if (r >= 3) t.push_back(ms);
+  }
+  std::sort(t.begin(), t.end());
+  return t[0];
+}
+
+int main() {
+  const long m = 25L << 20, nnz = m * 10;  // 3 GB of col+val, 200 MB of y
+  int *col;
+  double *val, *y, *out;
+  CK(hipMalloc(&col, nnz * 4));
+  CK(hipMalloc(&val, nnz * 8));
+  CK(hipMalloc(&y, m * 8));
+  CK(hipMalloc(&out, 64));
+  CK(hipMemset(col, 0, nnz * 4));
+  CK(hipMemset(val, 0, nnz * 8));
+  const unsigned grid = (unsigned)(m / 64 / 4);
+  const double rbytes = (double)nnz * 12;
+#define RUN(L, S, ST, name)                                                                     \
+  do {                                                                                          \
+    const float ms = time_ms([&] { hipLaunchKernelGGL((probe<L, S, ST>), dim3(grid), dim3(256), \
+                                                      0, 0, col, val, y, nnz, out); }, 10);     \
+    printf("{\"variant\": \"%s\", \"load_aux\": %d, \"store_aux\": %d, \"ms\": %.4f, \"GBps\": %.0f}\n", \
+           name, L, S, ms, (rbytes + (ST ? m * 8.0 : 0.0)) / ms * 1e-6);                        \
+    fflush(stdout);                                                                             \
+  } while (0)
+  RUN(0, 0, false, "base");
+  RUN(0, 0, true, "+y");
+  RUN(0, 2, true, "+y st.nt");
+  RUN(0, 16, true, "+y st.sc1");
+  RUN(0, 17, true, "+y st.sc0sc1");
+  RUN(0, 19, true, "+y st.sc0sc1nt");
+  RUN(2, 0, false, "ld.nt base");
+  RUN(2, 0, true, "ld.nt +y");
+  RUN(2, 2, true, "ld.nt +y st.nt");
+  RUN(16, 0, false, "ld.sc1 base");
+  RUN(16, 0, true, "ld.sc1 +y");
+  RUN(18, 0, true, "ld.sc1nt +y");
+  RUN(17, 0, true, "ld.sc0sc1 +y");
+  RUN(3, 0, true, "ld.sc0nt +y");
+  RUN(0, 0, true, "+y");
+  RUN(0, 0, false, "base");
+  CK(hipGetLastError());
+  return 0;
+}

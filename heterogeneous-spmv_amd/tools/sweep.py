@@ -116,6 +116,8 @@ def variants(cfg, A, maps, full=False):
     v.append(("stream-auto-xcd", dict(kernel="stream", xcd_remap=True), None))
     v.append((tag3 + "-auto-xcd", dict(kernel="csr3", xcd_remap=True), m3))
     v.append(("stream-auto-nt", dict(kernel="stream", nontemporal=True), None))
+    v.append(("stream-auto-c32", dict(kernel="stream", col16=False), None))
+    v.append((tag3 + "-auto-c32", dict(kernel="csr3", col16=False), m3))
     if cfg == "c5":
         v.append(("stream-nosplit", dict(kernel="stream", split_rows=False), None))
     return v
@@ -143,6 +145,21 @@ def group_variants(A):
     return v
 
 
+def c16_variants(A, maps):
+    """16-bit column offsets (default) vs 32-bit columns, over chunk sizes."""
+    d = A.nnz / A.m
+    m3 = maps if maps is not None else hspmv.build_csr3_maps(A, *hspmv.csr3_params(d, "mi355x"))
+    v = []
+    for c16 in (True, False):
+        t = "" if c16 else "-c32"
+        for u in (0, 2, 3, 4, 6, 8):
+            tag = f"-u{u}" if u else "-auto"
+            v.append((f"stream{tag}{t}", dict(kernel="stream", chunk_u=u, col16=c16), None))
+        v.append((f"csr3-auto{t}", dict(kernel="csr3", col16=c16), m3))
+        v.append((f"stream-auto-nt{t}", dict(kernel="stream", nontemporal=True, col16=c16), None))
+    return v
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c2,c3,c4,c5")
@@ -150,7 +167,7 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--out", default="")
     ap.add_argument("--quick", action="store_true", help="only stream u4/u6 + csr3 auto")
-    ap.add_argument("--grid", default="main", choices=["main", "xcd", "groups"],
+    ap.add_argument("--grid", default="main", choices=["main", "xcd", "groups", "c16"],
                     help="xcd: the XCD chunk grid (blocks per XCD turn) at the auto chunk size")
     a = ap.parse_args()
     import oracle
@@ -165,7 +182,8 @@ def main():
               file=sys.stderr, flush=True)
         ops = []
         vs = {"main": lambda: variants(cfg, A, maps), "xcd": lambda: xcd_variants(A, maps),
-              "groups": lambda: group_variants(A)}[a.grid]()
+              "groups": lambda: group_variants(A),
+              "c16": lambda: c16_variants(A, maps)}[a.grid]()
         if a.quick:
             vs = [v for v in vs if v[0] in ("stream-u4", "stream-u6", "stream-u8", "stream-auto",
                                           "stream-auto-noxcd", "csr3-auto", "csr3-mi355x-auto")]
@@ -201,7 +219,8 @@ def main():
                    "gflops_min": round(2 * A.nnz / tmin * 1e-9, 1), "frac_peak": round(b / tmin * 1e-9 / PEAK, 4),
                    "chunk_u": op.info["chunk_u"], "waves_per_block": op.info["waves_per_block"],
                    "n_split_rows": op.info["n_split_rows"], "xcd_chunk": op.info["xcd_remap"],
-                   "groups": op.info["groups_per_wave"],
+                   "groups": op.info["groups_per_wave"], "col16": op.info["col16"],
+                   "format_gbps_min": round(op.info["format_bytes"] / tmin * 1e-9, 1),
                    "desc": desc}
             lines.append(rec)
             print(json.dumps(rec), flush=True)

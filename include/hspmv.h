@@ -118,6 +118,11 @@ typedef struct {
   int32_t groups_per_wave; /* STREAM: 64-row groups one wave walks        */
   int64_t x_entries;  /* distinct columns referenced = x entries one SpMV
                          must read (summed over GPUs); alg_bytes uses it    */
+  double format_bytes; /* bytes the device format actually moves per SpMV
+                          (< alg_bytes with 16-bit column offsets)          */
+  int32_t col16;      /* 0 = 32-bit columns; 1 + p = 16-bit column offsets
+                         plus p high-bit planes (see HSPMV_FLAG_NO_COL16)   */
+  int32_t pad_;
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
@@ -134,6 +139,8 @@ typedef struct hspmv_handle hspmv_handle;
 #define HSPMV_LANES_SHIFT 4
 #define HSPMV_LANES(l) ((unsigned)(l) << HSPMV_LANES_SHIFT)
 #define HSPMV_LANES_MASK (0x7Fu << HSPMV_LANES_SHIFT)
+#define HSPMV_FLAG_NO_COL16 (1u << 11)    /* keep 32-bit column indices in
+                                             the row kernels (see below)   */
 #define HSPMV_FLAG_NONTEMPORAL (1u << 12) /* nt loads for val/col streams  */
 #define HSPMV_FLAG_DEVICE_PTRS (1u << 13) /* A/maps are device pointers on
                                              the target device (borrowed)  */
@@ -151,6 +158,8 @@ typedef struct hspmv_handle hspmv_handle;
                                           col/val loads one chunk ahead   */
 #define HSPMV_FLAG_XCD_REMAP (1u << 22) /* force the XCD-contiguous block
                                            order whatever the size         */
+#define HSPMV_FLAG_COL16 (1u << 23)     /* force 16-bit column offsets
+                                           whenever p <= 8 (see below)     */
 /* Explicit XCD chunk: HSPMV_XCD_CHUNK(s), s a power of two >= 1: each XCD
  * takes s consecutive blocks in turn (1 = dispatch order).  Overrides the
  * two flags above; 0 = automatic. */
@@ -160,6 +169,16 @@ typedef struct hspmv_handle hspmv_handle;
  * next group's row pointers are loaded while this one streams.  0 = auto. */
 #define HSPMV_GROUPS_SHIFT 29
 #define HSPMV_GROUPS(g) ((unsigned)(__builtin_ctz((unsigned)(g)) + 1) << HSPMV_GROUPS_SHIFT)
+/* 16-bit column offsets (default when the matrix allows it): at handle
+ * creation the column indices are re-encoded per 256-nonzero block as
+ * col = base[k / 256] + off16[k] + (p high bits from p bit-planes), with p
+ * the fewest bits that cover every block's column span (p = 0 for spans
+ * < 65536, e.g. banded matrices); the STREAM and CSR3 kernels then stream
+ * 2 + p/8 instead of 4 index bytes per nonzero.  Used by default when p <= 1
+ * and the matrix streams from HBM (> 192 MiB); measured slower otherwise.
+ * HSPMV_FLAG_COL16 forces them (any size, p <= 8).   Products and summation order are
+ * unchanged, so y is bit-identical.  HSPMV_FLAG_NO_COL16 turns it off;
+ * hspmv_info.col16 / format_bytes report what a handle uses. */
 
 /* ---------------------------------------------------------------- handle */
 /* Upload A (and optional CSR-3 maps) to num_gpus devices (0 = all visible).

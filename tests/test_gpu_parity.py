@@ -320,3 +320,56 @@ def test_borrowed_device_arrays():
     bad = hspmv._lib.Csr(A.m, A.n, A.nnz, rp.data_ptr(), 0, val.data_ptr(), 1)
     with pytest.raises(hspmv.HspmvError, match="E_INVALID"):
         hspmv.SpMV.from_device(bad, None, A, device=0)
+
+
+def _wide_random(m, n, per_row, seed):
+    rng = np.random.default_rng(seed)
+    cols = np.sort(rng.choice(n, size=(m, per_row), replace=True), axis=1)
+    rp = np.arange(0, m * per_row + 1, per_row, dtype=np.int32)
+    val = rng.uniform(-1, 1, m * per_row)
+    return hspmv.CsrMatrix(m, n, rp, cols.reshape(-1).astype(np.int32), val)
+
+
+def _band_random(m, per_row, half, seed):
+    """Rows with per_row sorted columns within +-half of the diagonal."""
+    rng = np.random.default_rng(seed)
+    cols = np.arange(m)[:, None] + rng.integers(-half, half + 1, size=(m, per_row))
+    cols = np.sort(np.clip(cols, 0, m - 1), axis=1)
+    rp = np.arange(0, m * per_row + 1, per_row, dtype=np.int32)
+    return hspmv.CsrMatrix(m, m, rp, cols.reshape(-1).astype(np.int32),
+                           rng.uniform(-1, 1, m * per_row))
+
+
+def test_col16_offsets_bitwise_and_fallback():
+    """16-bit column offsets (+ p high-bit planes; forced here, p <= 8) give
+    the same y bit for bit as 32-bit columns, through STREAM, CSR3, prefetch
+    and split rows; p grows with the column span of a 256-nonzero block, and
+    a matrix needing more than 8 planes keeps 32-bit columns.  By default
+    these small (Infinity-Cache-resident) matrices keep 32-bit columns."""
+    cases = [(gen.laplace2d(300, 200), 1),                        # spans < 65536
+             (gen.stencil27(20), 1),
+             (gen.banded(30000, per_row=10, half=32, seed=5), 1),
+             (_band_random(150000, 10, 50000, 6), 2),               # 1 plane
+             (gen.powerlaw(200000, seed=3, dtype=np.float64), 3),     # 2 planes
+             (_split_row_matrix(), None),
+             (_wide_random(2000, 1 << 25, 40, 4), 0)]                 # 10 planes: off
+    for A, want in cases:
+        x = gen.rand_x(A.n, 9)
+        maps = hspmv.build_csr3_maps(A, 20, 10)
+        for kw, mp in [(dict(kernel="stream"), None), (dict(kernel="stream", prefetch=True), None),
+                       (dict(kernel="csr3"), maps), (dict(kernel="stream", chunk_u=2), None)]:
+            y16, i16 = gpu_spmv(A, x, mp, col16=True, **kw)
+            y32, i32 = gpu_spmv(A, x, mp, col16=False, **kw)
+            assert i32["col16"] == 0 and i32["format_bytes"] == i32["alg_bytes"]
+            if want is not None:
+                assert i16["col16"] == want, (kw, i16["col16"], want)
+            if i16["col16"]:
+                assert i16["format_bytes"] < i16["alg_bytes"]
+            assert np.array_equal(y16, y32), kw
+        check_fp64(A, x, y16, exact_rows=short_rows(A))
+        _, idef = gpu_spmv(A, x)
+        assert idef["col16"] == 0  # small: default keeps 32-bit columns
+    # the vector kernel always reads 32-bit columns
+    A = gen.laplace2d(100, 100)
+    _, iv = gpu_spmv(A, gen.rand_x(A.n, 1), kernel="vector", col16=True)
+    assert iv["col16"] == 0
