@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <chrono>
 #include <memory>
@@ -53,6 +54,8 @@ struct Shard {
   uint16_t *d_c16 = nullptr;  // 16-bit column offsets (owned even for borrowed A)
   int32_t *d_cbase = nullptr;
   uint64_t *d_cplanes = nullptr;
+  int32_t *d_xwin = nullptr;         // STREAM x windows {lo, w} per 64-row group
+  std::vector<int32_t> h_xwin;       // built at upload (host columns at hand)
   void *d_val = nullptr;
   void *d_x = nullptr;     // own x (n entries)
   void *d_y = nullptr;     // own y (m_shard entries) -- or a slice of d_yfull
@@ -119,6 +122,7 @@ void free_shard(Shard &s, bool borrowed) {
   (void)hipFree(s.d_c16);
   (void)hipFree(s.d_cbase);
   (void)hipFree(s.d_cplanes);
+  (void)hipFree(s.d_xwin);
   (void)hipFree(s.d_task);
   (void)hipFree(s.d_long_row);
   (void)hipFree(s.d_long_cstart);
@@ -223,6 +227,34 @@ int build_col16(Shard &s, const int32_t *col, int64_t nnz, int64_t m, int64_t n,
   return HSPMV_OK;
 }
 
+// x windows of the STREAM kernel's 64-row groups: {lo, w} with w = the
+// group's column span when it is at most kXWin entries (its x slice is then
+// staged in LDS and gathered from there), else 0.  Kept only when at least
+// half of the groups qualify (banded matrices); HSPMV_XWIN=0 disables.
+void build_xwin(Shard &s, const int32_t *rp, const int32_t *col, int64_t m) {
+  s.h_xwin.clear();
+  if (const char *e = getenv("HSPMV_XWIN"))
+    if (atoi(e) == 0) return;
+  const int64_t ng = (m + 63) / 64;
+  std::vector<int32_t> w((size_t)(2 * ng), 0);
+  int64_t fit = 0;
+  for (int64_t g = 0; g < ng; ++g) {
+    const int64_t k0 = rp[64 * g], k1 = rp[std::min(m, 64 * g + 64)];
+    if (k1 <= k0) continue;
+    int32_t lo = col[k0], hi = col[k0];
+    for (int64_t k = k0 + 1; k < k1; ++k) {
+      lo = std::min(lo, col[k]);
+      hi = std::max(hi, col[k]);
+    }
+    if ((int64_t)hi - lo + 1 <= kXWin) {
+      w[(size_t)(2 * g)] = lo;
+      w[(size_t)(2 * g + 1)] = hi - lo + 1;
+      ++fit;
+    }
+  }
+  if (2 * fit >= ng) s.h_xwin.swap(w);
+}
+
 // Uploads rows [r0, r1) of A (and the matching slice of the maps) to shard s.
 int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_t r0, int64_t r1,
                  int64_t ssr0, int64_t ssr1, int64_t y_rows_alloc, unsigned flags) {
@@ -258,6 +290,7 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
   s.A.val = s.d_val;
   bool c16 = false;
   if ((rc = build_col16(s, A->col_idx + k0, nnz, m, A->n, A->dtype, flags, &c16))) return rc;
+  build_xwin(s, rp.data(), A->col_idx + k0, m);
   if (mp && mp->n_ssr > 0) {
     const int64_t nssr = ssr1 - ssr0;
     const int64_t sr0 = mp->outer[ssr0], sr1 = mp->outer[ssr1];
@@ -334,6 +367,13 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)nb -
                   (double)s.A.n_cplanes * (double)(s.A.nnz - long_nnz) / 8.0;
   }
+  if (s.plan.kernel == kStream && !s.h_xwin.empty()) {
+    int rc;
+    if ((rc = dev_alloc(&s.d_xwin, 4 * s.h_xwin.size(), &s.bytes))) return rc;
+    HIP_TRY(hipMemcpy(s.d_xwin, s.h_xwin.data(), 4 * s.h_xwin.size(), hipMemcpyHostToDevice));
+    s.dp.xwin = s.d_xwin;
+  }
+  std::vector<int32_t>().swap(s.h_xwin);
   if (s.plan.kernel == kCsr3) {
     const std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
     const int64_t nssr = s.A.n_ssr;
@@ -454,6 +494,7 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
       s.x_entries = count_distinct_cols(cols.data(), A->nnz, A->n);
       bool c16 = false;
       if ((rc = build_col16(s, cols.data(), A->nnz, A->m, A->n, A->dtype, flags, &c16))) return rc;
+      build_xwin(s, rp.data(), cols.data(), A->m);
     }
     if (maps && maps->n_ssr > 0) {
       std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;

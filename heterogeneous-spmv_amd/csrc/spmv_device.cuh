@@ -149,34 +149,50 @@ __device__ __forceinline__ void group_bounds(const int32_t *__restrict__ rp, int
   end = valid ? rp[row + 1] : 0;
 }
 
+// Where a row kernel reads column indices from (DevCSR's col_idx, or the
+// 16-bit offsets + block bases + high-bit planes of the col16 format).
+struct ColSrc {
+  const int32_t *ci;
+  const uint16_t *c16;
+  const int32_t *cbase;
+  const uint64_t *cplanes;
+  int32_t n_planes, plane_words;
+};
+
+// x window of a STREAM group (XW): x[lo, lo + w) staged in the wave's LDS
+// slot `xs`, so the group's gathers are LDS reads; w == 0: global gathers.
+template <typename T>
+struct XWin {
+  const T *xs;
+  int32_t lo, w;
+};
+
 // One wavefront computes rows [g0, g1), g1 - g0 <= 64, whose bounds
 // (group_bounds) are in beg/end.  lds: kWave*U elements private to this
 // wave.  Per chunk of 64*U nonzeros: stage A loads col/val (coalesced),
-// stage B gathers x[col], stage C forms the products into LDS; then the row
-// sums.  PF (software pipelining): the next chunk's stage A is issued
-// between this chunk's stage B and C, so its latency overlaps the gather and
-// the sums.
-template <typename T, bool NT, int U, bool PF, bool C16>
+// stage B gathers x[col] (from the LDS window when XW and win.w > 0), stage
+// C forms the products into LDS; then the row sums.  PF (software
+// pipelining): the next chunk's stage A is issued between this chunk's
+// stage B and C, so its latency overlaps the gather and the sums.
+template <typename T, bool NT, int U, bool PF, bool C16, bool XW>
 __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, int32_t end,
-                                          int32_t long_t,
-                                          const int32_t *__restrict__ ci,
-                                          const uint16_t *__restrict__ c16,
-                                          const int32_t *__restrict__ cbase,
-                                          const uint64_t *__restrict__ cplanes,
-                                          int32_t n_planes, int32_t plane_words,
+                                          int32_t long_t, const ColSrc &cs,
                                           const T *__restrict__ val,
                                           const T *__restrict__ x,
                                           T *__restrict__ y, T *lds, int lane,
+                                          const XWin<T> &win,
                                           unsigned long long *ts = nullptr) {
   const int32_t row = g0 + lane;
   const bool valid = row < g1;
   const int32_t len = end - beg;
   (void)ts;
+  (void)win;
   const bool skip = len > long_t;
   const unsigned long long skipmask = __ballot(valid && skip);
   const unsigned long long coopmask = __ballot(valid && !skip && len > kSerialMax);
   const bool serial = valid && !skip && len <= kSerialMax;
   const gchar *xb = uniform_ptr(x);
+  const bool inwin = XW && win.w > 0;
   T acc = T(0);
   // Runs of consecutive non-split rows [a, b); normally one run = the group.
   int32_t a = g0;
@@ -191,7 +207,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
       const bool mine = serial && row >= a && row < b;
       int32_t col[U];
       T v[U];
-      const gchar *cb = C16 ? uniform_ptr(c16 + kb) : uniform_ptr(ci + kb);
+      const gchar *cb = C16 ? uniform_ptr(cs.c16 + kb) : uniform_ptr(cs.ci + kb);
       const gchar *vb = uniform_ptr(val + kb);
       // (A raw-buffer form -- SGPR descriptors bounded to the run, no
       // clamp VALU -- measured 0-2.5 % slower in one-process A/B runs,
@@ -208,16 +224,16 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
             const uint32_t e0 = (uint32_t)kb + (uint32_t)(c0 + min(u * kWave, last));
             const uint32_t ja = (uint32_t)kb + j;
             const uint32_t b0 = __builtin_amdgcn_readfirstlane(e0 >> kC16Shift);
-            const int64_t bp = sload_i64(cbase, (uint64_t)b0 * 4u);
+            const int64_t bp = sload_i64(cs.cbase, (uint64_t)b0 * 4u);
             const int32_t base = ((ja >> kC16Shift) == b0) ? (int32_t)bp : (int32_t)(bp >> 32);
             int32_t high = 0;
-            if (n_planes > 0) {  // wave-uniform; the two words a slice spans, by s_load
+            if (cs.n_planes > 0) {  // wave-uniform; the two words a slice spans, by s_load
               const uint32_t w0 = __builtin_amdgcn_readfirstlane(e0 >> 6);
               const bool first = (ja >> 6) == w0;
-              for (int p = 0; p < n_planes; ++p) {
-                const uint64_t at = ((uint64_t)p * (uint64_t)plane_words + w0) * 8u;
-                const uint64_t m0 = (uint64_t)sload_i64(cplanes, at);
-                const uint64_t m1 = (uint64_t)sload_i64(cplanes, at + 8u);
+              for (int p = 0; p < cs.n_planes; ++p) {
+                const uint64_t at = ((uint64_t)p * (uint64_t)cs.plane_words + w0) * 8u;
+                const uint64_t m0 = (uint64_t)sload_i64(cs.cplanes, at);
+                const uint64_t m1 = (uint64_t)sload_i64(cs.cplanes, at + 8u);
                 high |= (int32_t)(((first ? m0 : m1) >> (ja & 63u)) & 1u) << p;
               }
             }
@@ -238,13 +254,21 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         if (c0 == 0) HSPMV_TRACE(ts, 2, diag_stamp());
 #endif
         T xv[U], vv[U];
+        if (inwin) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if constexpr ((HSPMV_DIAG & 2) != 0)
-            xv[u] = T(col[u] & 1) + T(1);
-          else
-            xv[u] = ld_off<false, T>(xb, (uint32_t)col[u] * (uint32_t)sizeof(T));
-          vv[u] = v[u];
+          for (int u = 0; u < U; ++u) {
+            xv[u] = win.xs[col[u] - win.lo];
+            vv[u] = v[u];
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if constexpr ((HSPMV_DIAG & 2) != 0)
+              xv[u] = T(col[u] & 1) + T(1);
+            else
+              xv[u] = ld_off<false, T>(xb, (uint32_t)col[u] * (uint32_t)sizeof(T));
+            vv[u] = v[u];
+          }
         }
         if constexpr (PF) {
           __builtin_amdgcn_sched_barrier(0);
@@ -292,17 +316,34 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
   if (valid && !skip) y[row] = acc;
 }
 
+// Stages x[lo, lo + w) (w <= kXWin) into the wave's LDS window slot.  The
+// loads are contiguous (coalesced), unlike the gathers they replace.
+template <typename T>
+__device__ __forceinline__ void stage_xwin(T *xs, const T *__restrict__ x, int32_t lo, int32_t w,
+                                           int lane) {
+  const gchar *xb = uniform_ptr(x + lo);
+  T t[kXWin / kWave];
+#pragma unroll
+  for (int i = 0; i < kXWin / kWave; ++i) {
+    const int32_t e = min(i * kWave + lane, w - 1);
+    t[i] = ld_off<false, T>(xb, (uint32_t)e * (uint32_t)sizeof(T));
+  }
+#pragma unroll
+  for (int i = 0; i < kXWin / kWave; ++i) xs[i * kWave + lane] = t[i];
+  wave_sync();
+}
+
 // STREAM: wave w walks `groups` consecutive 64-row groups starting at row
 // w * groups * 64, loading the next group's row pointers before streaming
-// the current one.
-template <typename T, bool NT, int U, bool PF, bool C16>
+// the current one.  XW: groups whose x window (xwin[g] = {lo, w}) fits
+// kXWin entries gather from an LDS copy of it.
+template <typename T, bool NT, int U, bool PF, bool C16, bool XW>
 __global__ __launch_bounds__(256) void hspmv_csr_stream(
     int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups,
-    const int32_t *__restrict__ rp, const int32_t *__restrict__ ci,
-    const uint16_t *__restrict__ c16, const int32_t *__restrict__ cbase,
-    const uint64_t *__restrict__ cplanes, int32_t n_planes, int32_t plane_words,
+    const int32_t *__restrict__ rp, ColSrc cs, const int2 *__restrict__ xwin,
     const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[4 * kWave * U];
+  __shared__ T xlds[XW ? 4 * kXWin : 1];
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t blk = xcd_chunk_remap(blockIdx.x, gridDim.x, xcd_chunk);
@@ -328,10 +369,18 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
 #endif
   while (true) {
     const int32_t g1 = (int32_t)min<int64_t>(g0 + kWave, gend);
+    XWin<T> win{nullptr, 0, 0};
+    if constexpr (XW) {
+      const int64_t wv = sload_i64(xwin, (uint64_t)(g0 / kWave) * 8u);
+      win.lo = (int32_t)wv;
+      win.w = (int32_t)(wv >> 32);
+      win.xs = xlds + wid * kXWin;
+      if (win.w > 0) stage_xwin(xlds + wid * kXWin, x, win.lo, win.w, lane);
+    }
     int32_t nbeg = 0, nend = 0;
     if (g1 < gend) group_bounds(rp, g1, (int32_t)min<int64_t>(g1 + kWave, gend), lane, nbeg, nend);
-    wave_rows<T, NT, U, PF, C16>((int32_t)g0, g1, beg, end, long_t, ci, c16, cbase, cplanes,
-                                 n_planes, plane_words, val, x, y, my, lane, ts);
+    wave_rows<T, NT, U, PF, C16, XW>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
+                                     win, ts);
     ts = nullptr;  // trace the first group only
     if (g1 >= gend) break;
     g0 = g1;
@@ -343,10 +392,8 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
 template <typename T, bool NT, int U, bool PF, bool C16, int W>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, const int32_t *__restrict__ task_start,
-    const int32_t *__restrict__ rp, const int32_t *__restrict__ ci,
-    const uint16_t *__restrict__ c16, const int32_t *__restrict__ cbase,
-    const uint64_t *__restrict__ cplanes, int32_t n_planes, int32_t plane_words,
-    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
+    const int32_t *__restrict__ rp, ColSrc cs, const T *__restrict__ val,
+    const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[W * kWave * U];
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
@@ -357,14 +404,15 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
   const int32_t r1 = task_start[t + 1];
   if (r0 >= r1) return;
   T *my = lds + wid * kWave * U;
+  const XWin<T> nowin{nullptr, 0, 0};
   int32_t beg, end;
   group_bounds(rp, r0, min(r0 + kWave, r1), lane, beg, end);
   for (int32_t g0 = r0; g0 < r1; g0 += kWave) {
     const int32_t g1 = min(g0 + kWave, r1);
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
-    wave_rows<T, NT, U, PF, C16>(g0, g1, beg, end, long_t, ci, c16, cbase, cplanes, n_planes,
-                                 plane_words, val, x, y, my, lane);
+    wave_rows<T, NT, U, PF, C16, false>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
+                                        nowin);
     beg = nbeg;
     end = nend;
   }
@@ -372,22 +420,31 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
 
 // ------------------------------------------------------------------ launchers
 
+inline ColSrc col_src(const DevCSR &A) {
+  return ColSrc{A.col_idx, A.col16, A.cbase, A.cplanes, A.n_cplanes, A.cplane_words};
+}
+
 template <typename T, bool NT, int U, bool PF, bool C16>
 void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x, T *y,
                    hipStream_t st) {
   const T *val = static_cast<const T *>(A.val);
+  const ColSrc cs = col_src(A);
   if (p.kernel == kStream) {
-    hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16>), dim3((unsigned)p.blocks), dim3(256),
-                       0, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk, (int32_t)p.groups, A.row_ptr,
-                       A.col_idx, A.col16, A.cbase, A.cplanes, A.n_cplanes, A.cplane_words, val,
-                       x, y);
+    const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
+    if (xw)
+      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true>), dim3((unsigned)p.blocks),
+                         dim3(256), 0, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk,
+                         (int32_t)p.groups, A.row_ptr, cs, xw, val, x, y);
+    else
+      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false>), dim3((unsigned)p.blocks),
+                         dim3(256), 0, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk,
+                         (int32_t)p.groups, A.row_ptr, cs, xw, val, x, y);
     return;
   }
 #define HSPMV_CSR3(W)                                                                     \
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C16, W>), dim3((unsigned)p.blocks),        \
                      dim3(W * 64), 0, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,   \
-                     dp.task_start, A.row_ptr, A.col_idx, A.col16, A.cbase, A.cplanes,     \
-                     A.n_cplanes, A.cplane_words, val, x, y)
+                     dp.task_start, A.row_ptr, cs, val, x, y)
   switch (p.waves_per_block) {
     case 1: HSPMV_CSR3(1); break;
     case 2: HSPMV_CSR3(2); break;

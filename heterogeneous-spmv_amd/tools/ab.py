@@ -11,6 +11,7 @@ Rounds interleave the libraries; min and median kernel times are reported.
 import argparse
 import ctypes as C
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -45,22 +46,32 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    # each entry: path[@flags] (flags ORed with --flags for that handle)
-    entries = [(e.split("@")[0], int(e.split("@")[1]) if "@" in e else 0) for e in a.libs.split(",")]
+    # each entry: path[@flags][#VAR=VALUE] (flags ORed with --flags; the
+    # environment variable is set while that handle is created)
+    entries, envs = [], []
+    for e in a.libs.split(","):
+        e, _, env = e.partition("#")
+        envs.append(tuple(env.split("=", 1)) if env else None)
+        entries.append((e.split("@")[0], int(e.split("@")[1]) if "@" in e else 0))
     cache = {}
     libs = [cache.setdefault(p, load(p)) for p, _ in entries]
     extra = [f for _, f in entries]
-    names = [Path(p).parent.name + "/" + Path(p).name + (f"@{f}" if f else "") for p, f in entries]
+    names = [Path(p).parent.name + "/" + Path(p).name + (f"@{f}" if f else "") +
+             (f"#{v[0]}={v[1]}" if v else "") for (p, f), v in zip(entries, envs)]
     out = []
     for cfg in a.configs.split(","):
         A, maps, desc = build(cfg)
         x = gen.rand_x(A.n, 42).astype(A.val.dtype)
         cs, ms = A.c_struct(), (maps.c_struct() if maps is not None and a.kernel != "stream" else None)
         hs = []
-        for L, fx in zip(libs, extra):
+        for L, fx, env in zip(libs, extra, envs):
+            if env:
+                os.environ[env[0]] = env[1]
             h = C.c_void_p()
             rc = L.hspmv_create_on_device(C.byref(h), C.byref(cs), C.byref(ms) if ms else None, 0,
                                           None, _KERNELS[a.kernel] | a.flags | fx)
+            if env:
+                os.environ.pop(env[0], None)
             assert rc == 0, L.hspmv_last_error()
             assert L.hspmv_set_x(h, x.ctypes.data) == 0
             hs.append(h)
