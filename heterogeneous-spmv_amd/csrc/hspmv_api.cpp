@@ -161,8 +161,8 @@ constexpr double kMallResident = 192.0 * 1024 * 1024;  // same bound as the XCD 
 int build_col16(Shard &s, const int32_t *col, int64_t nnz, int64_t m, int64_t n, int dtype,
                 unsigned flags, bool *used) {
   *used = false;
-  if ((flags & HSPMV_FLAG_NO_COL16) || nnz == 0) return HSPMV_OK;
-  const bool forced = (flags & HSPMV_FLAG_COL16) != 0;
+  if (nnz == 0) return HSPMV_OK;
+  const bool forced = (flags & HSPMV_FLAG_COL16) != 0 && !(flags & HSPMV_FLAG_NO_COL16);
   const double sv = (double)dtype_size(dtype);
   if (!forced && (double)nnz * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv <= kMallResident)
     return HSPMV_OK;
@@ -192,6 +192,8 @@ int build_col16(Shard &s, const int32_t *col, int64_t nnz, int64_t m, int64_t n,
   for (int32_t v : span) maxspan = std::max(maxspan, v);
   int bits = 0;
   while (bits < 31 && (int64_t(1) << bits) <= maxspan) ++bits;
+  s.A.col_span_bits = std::max(1, bits);  // the planner's gather-regularity hint
+  if (flags & HSPMV_FLAG_NO_COL16) return HSPMV_OK;
   const int planes = std::max(0, bits - 16);
   if (planes > (forced ? kMaxC16PlanesForced : kMaxC16Planes)) return HSPMV_OK;
   const int64_t nw = (nnz + 63) / 64 + 1;  // +1: kernels load words in pairs

@@ -23,6 +23,7 @@ struct DevCSR {
   const int32_t *cbase = nullptr;
   const uint64_t *cplanes = nullptr;
   int32_t n_cplanes = 0, cplane_words = 0;
+  int32_t col_span_bits = 0;  // bits of the widest 256-nonzero block's column span (0 = unknown)
 };
 
 constexpr int kC16Shift = 8;  // 256 nonzeros per column-base block
@@ -62,6 +63,7 @@ struct LaunchPlan {
   int u = 8;               // STREAM/CSR3: elements per lane per LDS chunk
   bool nontemporal = false;
   bool prefetch = false;   // STREAM/CSR3: next chunk's col/val issued early
+  bool y_nt = false;       // STREAM/CSR3: nontemporal y stores
   int32_t xcd_chunk = 1;   // blocks per XCD turn (1 = dispatch order; see xcd_chunk_remap)
   int32_t groups = 1;      // STREAM: 64-row groups per wave (next group's rp prefetched)
   int64_t blocks = 0;

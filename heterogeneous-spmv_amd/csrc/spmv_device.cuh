@@ -180,7 +180,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
                                           const T *__restrict__ val,
                                           const T *__restrict__ x,
                                           T *__restrict__ y, T *lds, int lane,
-                                          const XWin<T> &win,
+                                          const XWin<T> &win, bool y_nt,
                                           unsigned long long *ts = nullptr) {
   const int32_t row = g0 + lane;
   const bool valid = row < g1;
@@ -313,7 +313,12 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
 #if (HSPMV_DIAG & 8)
   HSPMV_TRACE(ts, 5, diag_stamp());
 #endif
-  if (valid && !skip) y[row] = acc;
+  if (valid && !skip) {
+    if (y_nt)  // HBM-resident: streaming stores (bw_probe3/4: y writes cost ~20 % of time)
+      __builtin_nontemporal_store(acc, y + row);
+    else
+      y[row] = acc;
+  }
 }
 
 // Stages x[lo, lo + w) (w <= kXWin) into the wave's LDS window slot.  The
@@ -339,7 +344,7 @@ __device__ __forceinline__ void stage_xwin(T *xs, const T *__restrict__ x, int32
 // kXWin entries gather from an LDS copy of it.
 template <typename T, bool NT, int U, bool PF, bool C16, bool XW>
 __global__ __launch_bounds__(256) void hspmv_csr_stream(
-    int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups,
+    int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups, int32_t y_nt,
     const int32_t *__restrict__ rp, ColSrc cs, const int2 *__restrict__ xwin,
     const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[4 * kWave * U];
@@ -380,7 +385,7 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
     int32_t nbeg = 0, nend = 0;
     if (g1 < gend) group_bounds(rp, g1, (int32_t)min<int64_t>(g1 + kWave, gend), lane, nbeg, nend);
     wave_rows<T, NT, U, PF, C16, XW>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                     win, ts);
+                                     win, y_nt != 0, ts);
     ts = nullptr;  // trace the first group only
     if (g1 >= gend) break;
     g0 = g1;
@@ -391,7 +396,8 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
 
 template <typename T, bool NT, int U, bool PF, bool C16, int W>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
-    int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, const int32_t *__restrict__ task_start,
+    int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, int32_t y_nt,
+    const int32_t *__restrict__ task_start,
     const int32_t *__restrict__ rp, ColSrc cs, const T *__restrict__ val,
     const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[W * kWave * U];
@@ -412,7 +418,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
     wave_rows<T, NT, U, PF, C16, false>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                        nowin);
+                                        nowin, y_nt != 0);
     beg = nbeg;
     end = nend;
   }
@@ -434,17 +440,17 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
     if (xw)
       hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true>), dim3((unsigned)p.blocks),
                          dim3(256), 0, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk,
-                         (int32_t)p.groups, A.row_ptr, cs, xw, val, x, y);
+                         (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs, xw, val, x, y);
     else
       hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false>), dim3((unsigned)p.blocks),
                          dim3(256), 0, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk,
-                         (int32_t)p.groups, A.row_ptr, cs, xw, val, x, y);
+                         (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs, xw, val, x, y);
     return;
   }
 #define HSPMV_CSR3(W)                                                                     \
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C16, W>), dim3((unsigned)p.blocks),        \
                      dim3(W * 64), 0, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,   \
-                     dp.task_start, A.row_ptr, cs, val, x, y)
+                     (int32_t)p.y_nt, dp.task_start, A.row_ptr, cs, val, x, y)
   switch (p.waves_per_block) {
     case 1: HSPMV_CSR3(1); break;
     case 2: HSPMV_CSR3(2); break;

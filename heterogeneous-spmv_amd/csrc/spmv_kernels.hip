@@ -48,6 +48,8 @@
 // that only the explicit fma() calls (vector kernel, long rows) fuse.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "hspmv_internal.h"
 
 namespace hspmv {
@@ -200,7 +202,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_r
   (void)rp_host;
   LaunchPlan p;
   const unsigned k = flags & 0xFu;
-  p.nontemporal = (flags & (1u << 12)) != 0;
+  p.nontemporal = (flags & (1u << 12)) != 0;  // HSPMV_FLAG_NONTEMPORAL
   p.prefetch = (flags & (1u << 21)) != 0;  // HSPMV_FLAG_PREFETCH
   const double d = A.m ? (double)A.nnz / (double)A.m : 0.0;
   // XCD block order: a contiguous eighth of the rows per XCD keeps x in that
@@ -271,6 +273,17 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_r
     chunk = per_xcd > 1 ? (int32_t)per_xcd : 1;
   }
   p.xcd_chunk = chunk;
+  // HBM-resident matrices: nontemporal y stores; and nontemporal col/val
+  // streams when the x gather is irregular (column spans of 2^18+ per
+  // 256-nonzero block) and x exceeds an XCD's 4 MiB L2, so the streamed
+  // bytes do not evict x (C5: -5 %; banded C3/C4: +3-7 %, left off).
+  // HSPMV_YNT / HSPMV_NT (0/1) override, for A/B runs.
+  const bool hbm = footprint > 192.0 * 1024 * 1024;
+  p.y_nt = hbm;
+  if (!p.nontemporal && hbm && A.col_span_bits > 17 && (double)A.n * sv > 4.0 * 1024 * 1024)
+    p.nontemporal = true;
+  if (const char *e = getenv("HSPMV_YNT")) p.y_nt = atoi(e) != 0;
+  if (const char *e = getenv("HSPMV_NT")) p.nontemporal = atoi(e) != 0;
   return p;
 }
 
