@@ -382,13 +382,37 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     const int W = s.plan.waves_per_block;
     std::vector<int32_t> ts((size_t)(nssr * W + 1));
     for (int64_t b = 0; b < nssr; ++b) {
+      // The super-super-row's rows [R0, R1) go to its W waves in contiguous
+      // ranges: wave w starts at the super-row boundary nearest above w/W of
+      // the nonzeros (the reference's nnz balance on its multilevel maps),
+      // unless that makes the previous range longer than one 64-row wave
+      // pass or leaves the later waves more than 64 rows each -- then the cut
+      // moves to the row that satisfies both (cap = ceil(rows / W) instead of
+      // 64 when the SSR has more than W * 64 rows).  No range is empty while rows
+      // remain.  (Pure super-row cuts left 15 % of the tasks empty beside
+      // doubled ones on a 64-row grouping; pure row cuts lost 7 % on C3's
+      // reference grouping; profiles/r01_ab_csr3_tasks.jsonl.)
       const int32_t s0 = o[b], s1 = o[b + 1];
-      const int64_t k0 = rp[in[s0]], k1 = rp[in[s1]];
-      int32_t sr = s0;
-      for (int w = 0; w < W; ++w) {
+      const int32_t R0 = in[s0], R1 = in[s1];
+      const int64_t k0 = rp[R0], k1 = rp[R1];
+      int32_t sr = s0, r = R0, prev = R0;
+      ts[(size_t)(b * W)] = R0;
+      for (int w = 1; w < W; ++w) {
         const int64_t target = k0 + (k1 - k0) * w / W;
         while (sr < s1 && rp[in[sr]] < target) ++sr;
-        ts[(size_t)(b * W + w)] = in[w == 0 ? s0 : sr];
+        while (r < R1 && rp[r] < target) ++r;
+        // a wave pass is 64 rows; an SSR with more than W*64 rows is split
+        // evenly instead (one long task would set the kernel's tail)
+        const int64_t cap = (int64_t)(R1 - R0) <= 64LL * W ? 64 : ((int64_t)(R1 - R0) + W - 1) / W;
+        const int64_t lo = std::max<int64_t>((int64_t)R1 - (int64_t)(W - w) * cap, prev + 1);
+        const int64_t hi = std::min<int64_t>((int64_t)prev + cap, R1);
+        int64_t st = in[sr];
+        if (st < lo || st > hi) st = std::min<int64_t>(std::max<int64_t>(r, lo), hi);
+        st = std::min<int64_t>(std::max<int64_t>(st, std::min<int64_t>(prev + 1, R1)), R1);
+        ts[(size_t)(b * W + w)] = (int32_t)st;
+        prev = (int32_t)st;
+        r = std::max(r, prev);
+        while (sr < s1 && in[sr] < prev) ++sr;
       }
     }
     ts[(size_t)(nssr * W)] = (int32_t)m;
@@ -412,7 +436,10 @@ int finish_shard(Shard &s, int dtype, unsigned flags, void *stream) {
   }
   HIP_TRY(hipEventCreate(&s.ev0));
   HIP_TRY(hipEventCreate(&s.ev1));
-  s.plan = plan_launch(s.A, dtype, flags, s.mean_rows_per_ssr, s.h_rp.data());
+  // CSR-3 block size from the mean rows per super-super-row (sizing on the
+  // 90th percentile doubled C3's waves for a 7-12 % loss, r01_ab_csr3_tasks)
+  const double ssr_rows = s.mean_rows_per_ssr;
+  s.plan = plan_launch(s.A, dtype, flags, ssr_rows, s.h_rp.data());
   int rc = build_plan_tables(s, dtype, flags);
   if (rc) return rc;
   s.x = s.d_x;

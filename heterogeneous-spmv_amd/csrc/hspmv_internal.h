@@ -64,6 +64,7 @@ struct LaunchPlan {
   bool nontemporal = false;
   bool prefetch = false;   // STREAM/CSR3: next chunk's col/val issued early
   bool y_nt = false;       // STREAM/CSR3: nontemporal y stores
+  int32_t dyn_lds = 0;     // extra dynamic LDS per block (occupancy experiments)
   int32_t xcd_chunk = 1;   // blocks per XCD turn (1 = dispatch order; see xcd_chunk_remap)
   int32_t groups = 1;      // STREAM: 64-row groups per wave (next group's rp prefetched)
   int64_t blocks = 0;
@@ -71,7 +72,7 @@ struct LaunchPlan {
 
 // Chooses kernel / lanes / block shape for a shard (host-side heuristic).
 // row_ptr_host: the shard's row pointer (m+1) on the host.
-LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_rows_per_ssr,
+LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_per_ssr,
                        const int32_t *row_ptr_host);
 
 // STREAM / CSR3 row kernels (stream_f32.hip / stream_f64.hip).

@@ -406,19 +406,34 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
   const int64_t blk = xcd_chunk_remap(blockIdx.x, gridDim.x, xcd_chunk);
   const int64_t t = blk * W + wid;
   if (t >= n_tasks) return;
-  const int32_t r0 = task_start[t];
-  const int32_t r1 = task_start[t + 1];
+#if (HSPMV_DIAG & 8)
+  const unsigned long long tb_stamp = diag_stamp();
+#endif
+  // both task bounds in one scalar load (K$), not a vector round trip
+  const int64_t tb = sload_i64(task_start, (uint64_t)t * 4u);
+  const int32_t r0 = (int32_t)tb;
+  const int32_t r1 = (int32_t)(tb >> 32);
   if (r0 >= r1) return;
   T *my = lds + wid * kWave * U;
   const XWin<T> nowin{nullptr, 0, 0};
+  unsigned long long *ts = nullptr;
+#if (HSPMV_DIAG & 8)
+  if (t < kTraceWaves) ts = g_trace + t * kTraceSlots;
+  HSPMV_TRACE(ts, 0, tb_stamp);
+  HSPMV_TRACE(ts, 6, (unsigned long long)(r1 - r0));
+#endif
   int32_t beg, end;
   group_bounds(rp, r0, min(r0 + kWave, r1), lane, beg, end);
+#if (HSPMV_DIAG & 8)
+  HSPMV_TRACE(ts, 1, diag_stamp());
+#endif
   for (int32_t g0 = r0; g0 < r1; g0 += kWave) {
     const int32_t g1 = min(g0 + kWave, r1);
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
     wave_rows<T, NT, U, PF, C16, false>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                        nowin, y_nt != 0);
+                                        nowin, y_nt != 0, ts);
+    ts = nullptr;
     beg = nbeg;
     end = nend;
   }
@@ -435,21 +450,22 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
                    hipStream_t st) {
   const T *val = static_cast<const T *>(A.val);
   const ColSrc cs = col_src(A);
+  const unsigned dyn = (unsigned)p.dyn_lds;  // occupancy experiments (HSPMV_DYNLDS)
   if (p.kernel == kStream) {
     const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
     if (xw)
       hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true>), dim3((unsigned)p.blocks),
-                         dim3(256), 0, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk,
+                         dim3(256), dyn, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk,
                          (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs, xw, val, x, y);
     else
       hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false>), dim3((unsigned)p.blocks),
-                         dim3(256), 0, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk,
+                         dim3(256), dyn, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk,
                          (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs, xw, val, x, y);
     return;
   }
 #define HSPMV_CSR3(W)                                                                     \
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C16, W>), dim3((unsigned)p.blocks),        \
-                     dim3(W * 64), 0, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,   \
+                     dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk, \
                      (int32_t)p.y_nt, dp.task_start, A.row_ptr, cs, val, x, y)
   switch (p.waves_per_block) {
     case 1: HSPMV_CSR3(1); break;

@@ -197,7 +197,7 @@ int pick_u(double nnz_per_pass, int dtype) {
 
 }  // namespace
 
-LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_rows_per_ssr,
+LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_per_ssr,
                        const int32_t *rp_host) {
   (void)rp_host;
   LaunchPlan p;
@@ -254,10 +254,10 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_r
     }
     case kCsr3: {
       p.lanes = kWave;
-      // ~64 rows per wave: one lane per row in the ordered sums
-      const double w = mean_rows_per_ssr / 64.0;
+      // ~64 rows per wave (one lane per row in the ordered sums)
+      const double w = rows_per_ssr / 64.0;
       p.waves_per_block = w >= 6.0 ? 8 : (w >= 3.0 ? 4 : (w >= 1.5 ? 2 : 1));
-      const double rows_per_task = mean_rows_per_ssr / p.waves_per_block;
+      const double rows_per_task = rows_per_ssr / p.waves_per_block;
       const double per_pass = (rows_per_task < 64.0 ? rows_per_task : 64.0) * d;
       p.u = forced_u ? forced_u : pick_u(per_pass < 64.0 * kLongRow ? per_pass : 64.0 * kLongRow, dtype);
       p.blocks = A.n_ssr;
@@ -284,6 +284,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double mean_r
     p.nontemporal = true;
   if (const char *e = getenv("HSPMV_YNT")) p.y_nt = atoi(e) != 0;
   if (const char *e = getenv("HSPMV_NT")) p.nontemporal = atoi(e) != 0;
+  if (const char *e = getenv("HSPMV_DYNLDS")) p.dyn_lds = atoi(e);
   return p;
 }
 

@@ -44,6 +44,25 @@ def build(cfg):
         A = gen.stencil27(125)
         maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "volta"))
         return A, maps, "C3 27-pt 125^3 RCM CSR-3 fp64 (ssrs=20, srs=10)"
+    if cfg == "c3m":  # C3's matrix with the MI355X CSR-3 grouping (64, 4)
+        A = gen.stencil27(125)
+        maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
+        return A, maps, "C3 27-pt 125^3 RCM CSR-3 fp64 (mi355x grouping ssrs=64, srs=4)"
+    if cfg.startswith("c3s"):  # C3's matrix, CSR-3 grouping (ssrs, srs) = c3s<ssrs>x<srs>
+        ssrs, srs = (int(v) for v in cfg[3:].split("x"))
+        A = gen.stencil27(125)
+        maps = hspmv.build_csr3_maps(A, ssrs, srs)
+        return A, maps, f"C3 27-pt 125^3 RCM CSR-3 fp64 (ssrs={ssrs}, srs={srs})"
+    if cfg in ("c3g", "c4g"):  # CSR-3 maps with exactly STREAM's 64-row groups, 4 per block
+        A = gen.stencil27(125) if cfg == "c3g" else hdist.build_shard("c4", 0, 8).A
+        inner = np.append(np.arange(0, A.m, 64), A.m).astype(np.int32)
+        nsr = len(inner) - 1
+        outer = np.append(np.arange(0, nsr, 4), nsr).astype(np.int32)
+        return A, hspmv.Csr3Maps(outer, inner), f"{cfg}: CSR-3 maps = 64-row groups x 4"
+    if cfg.startswith("c4s"):  # C4's shard, CSR-3 grouping c4s<ssrs>x<srs>
+        ssrs, srs = (int(v) for v in cfg[3:].split("x"))
+        sh = hdist.build_shard("c4", 0, 8)
+        return sh.A, hspmv.build_csr3_maps(sh.A, ssrs, srs), f"C4 shard CSR-3 ({ssrs}, {srs})"
     if cfg == "c4":
         sh = hdist.build_shard("c4", 0, 8)
         return sh.A, None, "C4 banded 2e7 rows, rank-0 shard of 8 (2.5M rows) fp64"

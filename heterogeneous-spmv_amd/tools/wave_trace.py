@@ -36,6 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c4,c3")
     ap.add_argument("--u", type=int, default=0)
+    ap.add_argument("--kernel", default="stream")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     assert "diag8" in os.environ.get("HSPMV_LIB", ""), "set HSPMV_LIB to the diag8 build"
@@ -43,8 +44,8 @@ def main():
     L.hspmv_diag_trace.argtypes = [C.c_void_p, C.c_size_t]
     out = []
     for cfg in a.configs.split(","):
-        A, _, desc = build(cfg)
-        op = hspmv.SpMV(A, kernel="stream", chunk_u=a.u)
+        A, maps, desc = build(cfg)
+        op = hspmv.SpMV(A, maps if a.kernel == "csr3" else None, kernel=a.kernel, chunk_u=a.u)
         op.set_x(gen.rand_x(A.n, 42).astype(A.val.dtype))
         t = op.run(warmup=3, iters=10)
         assert L.hspmv_diag_trace_clear() == 0
@@ -57,7 +58,7 @@ def main():
         d = {k: tr[:, i + 1] - tr[:, i] for i, k in enumerate(["rp", "colval", "gather", "sums"])}
         d["rest"] = tr[:, 5] - tr[:, 4]
         d["life"] = tr[:, 5] - tr[:, 0]
-        rec = {"config": cfg, "desc": desc, "t_min_us": t["t_min"] * 1e6, "waves": int(len(tr)),
+        rec = {"config": cfg, "kernel": a.kernel, "desc": desc, "t_min_us": t["t_min"] * 1e6, "waves": int(len(tr)),
                "chunks_mean": float(tr[:, 7].mean()), "info_u": op.info["chunk_u"],
                "phases_cycles": {k: q(v) for k, v in d.items()},
                "mean_cycles": {k: float(v.mean()) for k, v in d.items()}}
