@@ -382,37 +382,27 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     const int W = s.plan.waves_per_block;
     std::vector<int32_t> ts((size_t)(nssr * W + 1));
     for (int64_t b = 0; b < nssr; ++b) {
-      // The super-super-row's rows [R0, R1) go to its W waves in contiguous
-      // ranges: wave w starts at the super-row boundary nearest above w/W of
-      // the nonzeros (the reference's nnz balance on its multilevel maps),
-      // unless that makes the previous range longer than one 64-row wave
-      // pass or leaves the later waves more than 64 rows each -- then the cut
-      // moves to the row that satisfies both (cap = ceil(rows / W) instead of
-      // 64 when the SSR has more than W * 64 rows).  No range is empty while rows
-      // remain.  (Pure super-row cuts left 15 % of the tasks empty beside
-      // doubled ones on a 64-row grouping; pure row cuts lost 7 % on C3's
-      // reference grouping; profiles/r01_ab_csr3_tasks.jsonl.)
       const int32_t s0 = o[b], s1 = o[b + 1];
-      const int32_t R0 = in[s0], R1 = in[s1];
-      const int64_t k0 = rp[R0], k1 = rp[R1];
-      int32_t sr = s0, r = R0, prev = R0;
-      ts[(size_t)(b * W)] = R0;
-      for (int w = 1; w < W; ++w) {
+      const int64_t k0 = rp[in[s0]], k1 = rp[in[s1]];
+      // wave w starts at the first super-row reaching w/W of the nonzeros,
+      // but strictly after wave w-1's start while super-rows remain: two
+      // waves never share a start (an empty task beside a doubled one was
+      // 15 % of the tasks on a 64-row grouping: 144 -> 129 us there).
+      // Row-granular cuts capped at 64 rows per wave measured 7-30 % slower
+      // on C3's groupings (long tails where an SSR exceeds W*64 rows);
+      // profiles/r01_ab_csr3_tasks.jsonl.
+      int32_t sr = s0, prev = s0 - 1;
+      for (int w = 0; w < W; ++w) {
         const int64_t target = k0 + (k1 - k0) * w / W;
         while (sr < s1 && rp[in[sr]] < target) ++sr;
-        while (r < R1 && rp[r] < target) ++r;
-        // a wave pass is 64 rows; an SSR with more than W*64 rows is split
-        // evenly instead (one long task would set the kernel's tail)
-        const int64_t cap = (int64_t)(R1 - R0) <= 64LL * W ? 64 : ((int64_t)(R1 - R0) + W - 1) / W;
-        const int64_t lo = std::max<int64_t>((int64_t)R1 - (int64_t)(W - w) * cap, prev + 1);
-        const int64_t hi = std::min<int64_t>((int64_t)prev + cap, R1);
-        int64_t st = in[sr];
-        if (st < lo || st > hi) st = std::min<int64_t>(std::max<int64_t>(r, lo), hi);
-        st = std::min<int64_t>(std::max<int64_t>(st, std::min<int64_t>(prev + 1, R1)), R1);
-        ts[(size_t)(b * W + w)] = (int32_t)st;
-        prev = (int32_t)st;
-        r = std::max(r, prev);
-        while (sr < s1 && in[sr] < prev) ++sr;
+        int32_t st = w == 0 ? s0 : sr;
+        if (st <= prev) st = prev + 1;
+        const int32_t latest = s1 - (W - w);  // leave one super-row per later wave
+        if (st > latest) st = std::max(prev + 1, latest);
+        if (st > s1) st = s1;
+        ts[(size_t)(b * W + w)] = in[st];
+        prev = st;
+        sr = std::max(sr, st);
       }
     }
     ts[(size_t)(nssr * W)] = (int32_t)m;
