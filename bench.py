@@ -244,13 +244,15 @@ def main():
             "config": {"workload": f"{args.config}: {shard.name}", "m": shard.m_global,
                        "nnz": shard.nnz_global, "rows_per_gpu": int(A.m),
                        "kernel": info["kernel_name"], "lanes": info["lanes"],
-                       "nontemporal": bool(args.nt), "parallelism": f"row-range x{world}"},
+                       "nontemporal": bool(args.nt), "parallelism": f"row-range x{world}",
+                       "workload_key": workload_key, "col16": info["col16"]},
             "gbps_alg": round(alg_total / step_s * 1e-9, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": (traffic["hbm_bytes_per_launch"] if traffic else None),
                          "kernel": f"hspmv_csr_{info['kernel_name']}<double>",
                          "alg_bytes_per_launch": alg_local,
+                         "format_bytes_per_launch": info["format_bytes"],
                          "launch_us_events": round(ev_launch_s * 1e6, 3),
                          "traffic_source": (traffic["source"] if traffic else None)},
             "cold": {"launch_us": round(cold_s * 1e6, 3),
