@@ -44,6 +44,7 @@ struct Options {
   bool check = true;
   std::string dump_y;
   std::string params = "mi355x";
+  bool bandk = true;  // spmv-csrk on a .csr: band-k reorder (the reference's CSRk_Graph)
 };
 
 inline bool ends_with(const std::string &s, const char *suf) {
@@ -91,6 +92,8 @@ inline bool parse_options(int argc, char **argv, int first, Options &o) {
     } else if (a == "--dump-y") {
       const char *v = need("--dump-y"); if (!v) return false;
       o.dump_y = v;
+    } else if (a == "--file-order") {
+      o.bandk = false;
     } else if (a == "--params") {
       const char *v = need("--params"); if (!v) return false;
       o.params = v;
@@ -159,8 +162,11 @@ inline int die(const char *what) {
 }
 
 // Runs the timed protocol on an already-read matrix and prints the report.
+// perm (optional, m entries): A is the band-k permutation of the file's
+// matrix, row i = file row perm[i]; x is generated in file order and
+// permuted, and a dumped y is put back in file order.
 inline int run_and_report(const hspmv_csr_buf &A, const hspmv_csr3_buf *maps, int num_runs,
-                          const Options &o) {
+                          const Options &o, const int32_t *perm = nullptr) {
   hspmv_csr view = {A.m, A.n, A.nnz, A.row_ptr, A.col_idx, A.val, A.dtype};
   hspmv_csr3_maps mv = {0, 0, nullptr, nullptr};
   if (maps && maps->n_ssr > 0) mv = {maps->n_ssr, maps->n_sr, maps->outer, maps->inner};
@@ -169,6 +175,10 @@ inline int run_and_report(const hspmv_csr_buf &A, const hspmv_csr3_buf *maps, in
     return die("hspmv_create");
   std::vector<double> x64;
   fill_x(o, A.n, x64);
+  if (perm) {
+    std::vector<double> xf(x64);
+    for (int64_t i = 0; i < A.n; ++i) x64[(size_t)i] = xf[(size_t)perm[i]];
+  }
   std::vector<float> x32;
   const void *xp = x64.data();
   if (A.dtype == HSPMV_F32) {
@@ -195,8 +205,13 @@ inline int run_and_report(const hspmv_csr_buf &A, const hspmv_csr3_buf *maps, in
   std::vector<char> y(sv * (size_t)(A.m ? A.m : 1));
   if (hspmv_get_y(h, y.data()) != HSPMV_OK) return die("hspmv_get_y");
   if (!o.dump_y.empty()) {
+    std::vector<char> yf(y.size());
+    if (perm)  // back to the file's row order
+      for (int64_t i = 0; i < A.m; ++i) memcpy(&yf[sv * (size_t)perm[i]], &y[sv * (size_t)i], sv);
+    else
+      yf = y;
     FILE *fp = fopen(o.dump_y.c_str(), "wb");
-    if (!fp || fwrite(y.data(), sv, (size_t)A.m, fp) != (size_t)A.m) {
+    if (!fp || fwrite(yf.data(), sv, (size_t)A.m, fp) != (size_t)A.m) {
       fprintf(stderr, "cannot write %s\n", o.dump_y.c_str());
       return 1;
     }

@@ -7,8 +7,11 @@
 //       mi355x|mi100|volta picks the formula; default mi355x)
 //   spmv-csrk <file.csr3> <num_runs>
 //       maps read from the .csr3 file (reformat-csr-to-csr3 output)
-// The maps are built in file order (handCoarsen grouping, no RCM), so y is
-// in the file's row order; see DESIGN.md.
+// On a .csr the matrix goes through the reference's band-k build
+// (hspmv_build_csr3_bandk: hand-coarsening + RCM per coarse level + symmetric
+// permutation, CSRk_Graph::putInCSRkFormat) -- with the permutation applied
+// to the matrix AND x, which the reference's GPU driver misses (SURVEY.md
+// Appendix A item 3); --file-order keeps the file's row order (maps only).
 #include "cli_common.h"
 
 int main(int argc, char **argv) {
@@ -34,6 +37,7 @@ int main(int argc, char **argv) {
   }
   hspmv_csr_buf A;
   hspmv_csr3_buf maps;
+  std::vector<int32_t> perm;  // band-k: permuted row i = file row perm[i]
   if (cli::read_matrix(argv[1], o.dtype, A, maps) != HSPMV_OK) return cli::die("read");
   if (A.dtype != o.dtype) {
     fprintf(stderr, "matrix file holds dtype %d, requested %d\n", A.dtype, o.dtype);
@@ -48,14 +52,23 @@ int main(int argc, char **argv) {
     printf("using ssrs %d, srs %d\n", ssrs, srs);
     hspmv_csr view = {A.m, A.n, A.nnz, A.row_ptr, A.col_idx, A.val, A.dtype};
     auto tic = std::chrono::steady_clock::now();
-    if (hspmv_build_csr3_maps(&view, ssrs, srs, &maps) != HSPMV_OK) return cli::die("build maps");
+    if (o.bandk && A.m == A.n) {
+      hspmv_csr_buf P;
+      perm.resize((size_t)A.m);
+      if (hspmv_build_csr3_bandk(&view, ssrs, srs, &P, &maps, perm.data()) != HSPMV_OK)
+        return cli::die("band-k build");
+      hspmv_free_csr(&A);
+      A = P;
+    } else if (hspmv_build_csr3_maps(&view, ssrs, srs, &maps) != HSPMV_OK) {
+      return cli::die("build maps");
+    }
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - tic).count();
     printf("%s reordered in %g seconds.\n", argv[1], dt);
   }
   printf("In CSR-k format.\n");
   printf("super-super-rows %lld super-rows %lld rows %lld nnz %lld\n", (long long)maps.n_ssr,
          (long long)maps.n_sr, (long long)A.m, (long long)A.nnz);
-  const int rc = cli::run_and_report(A, &maps, num_runs, o);
+  const int rc = cli::run_and_report(A, &maps, num_runs, o, perm.empty() ? nullptr : perm.data());
   hspmv_free_csr3(&maps);
   hspmv_free_csr(&A);
   return rc;

@@ -141,6 +141,8 @@ SIGNATURES = {
     "hspmv_free_csr": (None, [C.POINTER(CsrBuf)]),
     "hspmv_free_csr3": (None, [C.POINTER(Csr3Buf)]),
     "hspmv_build_csr3_maps": (C.c_int, [C.POINTER(Csr), C.c_int, C.c_int, C.POINTER(Csr3Buf)]),
+    "hspmv_build_csr3_bandk": (C.c_int, [C.POINTER(Csr), C.c_int, C.c_int, C.POINTER(CsrBuf),
+                                         C.POINTER(Csr3Buf), _P]),
     "hspmv_csr3_params": (C.c_int, [C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hspmv_partition_rows": (C.c_int, [C.c_int64, _P, C.POINTER(Csr3Maps), C.c_int, _P]),
     "hspmv_alg_bytes": (C.c_double, [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int64]),

@@ -194,6 +194,21 @@ def build_csr3_maps(A: CsrMatrix, ssrs: int, srs: int) -> Csr3Maps:
     return maps
 
 
+def build_csr3_bandk(A: CsrMatrix, ssrs: int, srs: int):
+    """The reference's band-k CSR-3 build (hspmv_build_csr3_bandk): returns
+    (A_perm, maps, perm) with A_perm = P A P^T, row i of A_perm = row perm[i]
+    of A; so A_perm @ x[perm] = (A @ x)[perm]."""
+    cs, buf, mbuf = A.c_struct(), _lib.CsrBuf(), _lib.Csr3Buf()
+    perm = np.empty(A.m, np.int32)
+    check(lib().hspmv_build_csr3_bandk(C.byref(cs), int(ssrs), int(srs), C.byref(buf),
+                                       C.byref(mbuf), _ptr(perm)), "build_csr3_bandk")
+    Ap = _take_csr(buf)
+    maps = _take_maps(mbuf)
+    if maps is None:
+        maps = Csr3Maps(np.zeros(1, np.int32), np.zeros(1, np.int32))
+    return Ap, maps, perm
+
+
 _FLAVOURS = {"volta": 0, "csr3-writer": 0, "mi100": 1, "mi355x": 2}
 
 

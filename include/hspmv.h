@@ -252,6 +252,17 @@ void hspmv_free_csr3(hspmv_csr3_buf *maps);
  * super-rows->super-super-rows size. */
 int hspmv_build_csr3_maps(const hspmv_csr *A, int ssrs, int srs,
                           hspmv_csr3_buf *out);
+/* The full band-k build of CSRk_Graph::putInCSRkFormat with k = 3 and HAND
+ * coarsening (BAND_k::preprocessingForSpMV, csrk.cu:1035-1262; reorderA
+ * :722-870): super-rows by the handCoarsen rule, RCM on the super-row graph,
+ * super-super-rows over the RCM order, RCM on that graph, uncoarsening into
+ * one symmetric permutation.  Outputs the permuted matrix (columns sorted
+ * per row; *A_out allocated, free with hspmv_free_csr), its maps (*maps_out,
+ * free with hspmv_free_csr3) and, if perm != NULL, perm[m]: new row i is row
+ * perm[i] of A (so y = P^T y_out, x_out[i] = x[perm[i]]).  A must be square.
+ * Replaces what reformat-csr-to-csr3 (spmv-auto.cpp:183-195) writes. */
+int hspmv_build_csr3_bandk(const hspmv_csr *A, int ssrs, int srs, hspmv_csr_buf *A_out,
+                           hspmv_csr3_buf *maps_out, int32_t *perm);
 /* Auto parameters.  flavour 0: the .csr3 writer / Volta formula
  * (reformat-csr-to-csr3/spmv-auto.cpp:154-173); 1: the MI100 driver formula
  * (hip/spmv-auto-mi100.cu:130-158); 2: this library's MI355X choice. */

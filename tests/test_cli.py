@@ -106,3 +106,21 @@ def test_bin_cache_through_cli(tmp_path):
     assert "Check: PASS" in p.stdout and "Kernel: csr3" in p.stdout
     p = run(BUILD / "spmv-csr", f, 5, "--x", "rand:9")
     assert "Check: PASS" in p.stdout and "Kernel: stream" in p.stdout
+
+
+@pytest.mark.gpu
+def test_spmv_csrk_bandk_reorders_and_restores_file_order(tmp_path):
+    # a .csr input goes through the band-k build (CSRk_Graph::putInCSRkFormat);
+    # x is permuted with the matrix and --dump-y writes y in the file's order
+    import hspmv
+    A = hspmv.read_csr(GOLDEN / "powerlaw1500.csr", np.float64)
+    x = gen.rand_x(A.n, 7)
+    y_ref = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    for extra in ([], ["--file-order"]):
+        out = tmp_path / "y.bin"
+        p = run(BUILD / "spmv-csrk", GOLDEN / "powerlaw1500.csr", 5, 20, 10, "--x", "rand:7",
+                "--dump-y", out, *extra)
+        assert "Check: PASS" in p.stdout and "reordered in" in p.stdout
+        y = np.fromfile(out, np.float64)
+        assert np.all(np.abs(y - y_ref) <= 1e-6 * np.abs(y_ref) + 1e-12 * absrow)
