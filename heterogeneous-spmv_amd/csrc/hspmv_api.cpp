@@ -56,6 +56,7 @@ struct Shard {
   uint64_t *d_cplanes = nullptr;
   int32_t *d_xwin = nullptr;         // STREAM x windows {lo, w} per 64-row group
   std::vector<int32_t> h_xwin;       // built at upload (host columns at hand)
+  std::vector<int32_t> h_xwin_t;     // the same per packed CSR-3 task
   void *d_val = nullptr;
   void *d_x = nullptr;     // own x (n entries)
   void *d_y = nullptr;     // own y (m_shard entries) -- or a slice of d_yfull
@@ -72,7 +73,7 @@ struct Shard {
           *d_chunk_k = nullptr;
   void *d_partials = nullptr;
   // host copies kept until the plan is built
-  std::vector<int32_t> h_rp, h_outer, h_inner;
+  std::vector<int32_t> h_rp, h_outer, h_inner, h_tasks;
 };
 
 }  // namespace
@@ -233,15 +234,64 @@ int build_col16(Shard &s, const int32_t *col, int64_t nnz, int64_t m, int64_t n,
 // group's column span when it is at most kXWin entries (its x slice is then
 // staged in LDS and gathered from there), else 0.  Kept only when at least
 // half of the groups qualify (banded matrices); HSPMV_XWIN=0 disables.
-void build_xwin(Shard &s, const int32_t *rp, const int32_t *col, int64_t m) {
-  s.h_xwin.clear();
+// CSR-3 task packing (the default CSR-3 plan): the super-rows of the inner
+// map, in order, are packed into wave tasks of at most one 64-row group
+// (the lanes of a wave's ordered sums); a super-row longer than 64 rows is
+// cut at 64-row steps.  Four consecutive tasks form a workgroup, so a
+// super-super-row spans as many waves as its rows need instead of a fixed W
+// per launch (handCoarsen's super-super-rows vary ~10x in rows).
+// HSPMV_CSR3_PLAN=ssr selects the workgroup-per-super-super-row plan.
+bool csr3_packed() {
+  const char *e = getenv("HSPMV_CSR3_PLAN");
+  return !(e && !strcmp(e, "ssr"));
+}
+
+void pack_csr3_tasks(Shard &s) {
+  constexpr int32_t kTaskRows = 64;  // one wave's lanes
+  const std::vector<int32_t> &in = s.h_inner;
+  const int32_t m = s.A.m;
+  std::vector<int32_t> &ts = s.h_tasks;
+  ts.clear();
+  ts.reserve((size_t)m / 32 + 2);
+  int32_t start = 0;
+  const int64_t nsr = (int64_t)in.size() - 1;
+  for (int64_t sr = 0; sr < nsr; ++sr) {
+    const int32_t r0 = in[(size_t)sr], r1 = in[(size_t)sr + 1];
+    if (r1 - start <= kTaskRows) continue;  // the super-row joins the open task
+    if (r0 > start) {                   // close the open task before it
+      ts.push_back(start);
+      start = r0;
+    }
+    while (r1 - start > kTaskRows) {  // a long super-row: 64-row steps
+      ts.push_back(start);
+      start += kTaskRows;
+    }
+  }
+  while (m - start > kTaskRows) {  // rows past the maps (none for validated maps)
+    ts.push_back(start);
+    start += kTaskRows;
+  }
+  if (start < m || ts.empty()) ts.push_back(start);
+  ts.push_back(m);
+}
+
+// x windows of row groups [starts[g], starts[g+1]) -- the 64-row groups of
+// STREAM when starts is null, the packed CSR-3 tasks otherwise: {lo, w} when
+// the group's columns span w <= kXWin entries, else {0, 0}.  Empty when
+// fewer than half the groups fit (HSPMV_XWIN=0 disables).
+std::vector<int32_t> xwin_table(const int32_t *rp, const int32_t *col, int64_t m,
+                                const std::vector<int32_t> *starts) {
+  std::vector<int32_t> w;
   if (const char *e = getenv("HSPMV_XWIN"))
-    if (atoi(e) == 0) return;
-  const int64_t ng = (m + 63) / 64;
-  std::vector<int32_t> w((size_t)(2 * ng), 0);
+    if (atoi(e) == 0) return w;
+  const int64_t ng = starts ? (int64_t)starts->size() - 1 : (m + 63) / 64;
+  if (ng <= 0) return w;
+  w.assign((size_t)(2 * ng), 0);
   int64_t fit = 0;
   for (int64_t g = 0; g < ng; ++g) {
-    const int64_t k0 = rp[64 * g], k1 = rp[std::min(m, 64 * g + 64)];
+    const int64_t r0 = starts ? (*starts)[(size_t)g] : 64 * g;
+    const int64_t r1 = starts ? (*starts)[(size_t)g + 1] : std::min(m, 64 * g + 64);
+    const int64_t k0 = rp[r0], k1 = rp[r1];
     if (k1 <= k0) continue;
     int32_t lo = col[k0], hi = col[k0];
     for (int64_t k = k0 + 1; k < k1; ++k) {
@@ -254,7 +304,17 @@ void build_xwin(Shard &s, const int32_t *rp, const int32_t *col, int64_t m) {
       ++fit;
     }
   }
-  if (2 * fit >= ng) s.h_xwin.swap(w);
+  if (2 * fit < ng) w.clear();
+  return w;
+}
+
+// Host-side tables that need the columns (built at upload, while they are
+// at hand): the CSR-3 packed tasks and the x windows of both row kernels.
+void build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, int64_t m) {
+  s.h_tasks.clear();
+  if (s.A.n_ssr > 0 && csr3_packed()) pack_csr3_tasks(s);
+  s.h_xwin = xwin_table(rp, col, m, nullptr);
+  s.h_xwin_t = s.h_tasks.empty() ? std::vector<int32_t>() : xwin_table(rp, col, m, &s.h_tasks);
 }
 
 // Uploads rows [r0, r1) of A (and the matching slice of the maps) to shard s.
@@ -292,7 +352,6 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
   s.A.val = s.d_val;
   bool c16 = false;
   if ((rc = build_col16(s, A->col_idx + k0, nnz, m, A->n, A->dtype, flags, &c16))) return rc;
-  build_xwin(s, rp.data(), A->col_idx + k0, m);
   if (mp && mp->n_ssr > 0) {
     const int64_t nssr = ssr1 - ssr0;
     const int64_t sr0 = mp->outer[ssr0], sr1 = mp->outer[ssr1];
@@ -312,6 +371,7 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
     s.A.inner = s.d_inner;
     s.mean_rows_per_ssr = nssr ? (double)m / (double)nssr : 0.0;
   }
+  build_row_tables(s, rp.data(), A->col_idx + k0, m);
   return HSPMV_OK;
 }
 
@@ -369,14 +429,22 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)nb -
                   (double)s.A.n_cplanes * (double)(s.A.nnz - long_nnz) / 8.0;
   }
-  if (s.plan.kernel == kStream && !s.h_xwin.empty()) {
+  const std::vector<int32_t> &xw = s.plan.kernel == kStream ? s.h_xwin : s.h_xwin_t;
+  if ((s.plan.kernel == kStream || (s.plan.kernel == kCsr3 && !s.h_tasks.empty())) && !xw.empty()) {
     int rc;
-    if ((rc = dev_alloc(&s.d_xwin, 4 * s.h_xwin.size(), &s.bytes))) return rc;
-    HIP_TRY(hipMemcpy(s.d_xwin, s.h_xwin.data(), 4 * s.h_xwin.size(), hipMemcpyHostToDevice));
+    if ((rc = dev_alloc(&s.d_xwin, 4 * xw.size(), &s.bytes))) return rc;
+    HIP_TRY(hipMemcpy(s.d_xwin, xw.data(), 4 * xw.size(), hipMemcpyHostToDevice));
     s.dp.xwin = s.d_xwin;
   }
   std::vector<int32_t>().swap(s.h_xwin);
-  if (s.plan.kernel == kCsr3) {
+  std::vector<int32_t>().swap(s.h_xwin_t);
+  if (s.plan.kernel == kCsr3 && !s.h_tasks.empty()) {
+    int rc;
+    if ((rc = dev_alloc(&s.d_task, 4 * s.h_tasks.size(), &s.bytes))) return rc;
+    HIP_TRY(hipMemcpy(s.d_task, s.h_tasks.data(), 4 * s.h_tasks.size(), hipMemcpyHostToDevice));
+    s.dp.task_start = s.d_task;
+    s.dp.n_tasks = (int32_t)(s.h_tasks.size() - 1);
+  } else if (s.plan.kernel == kCsr3) {
     const std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
     const int64_t nssr = s.A.n_ssr;
     const int W = s.plan.waves_per_block;
@@ -429,7 +497,8 @@ int finish_shard(Shard &s, int dtype, unsigned flags, void *stream) {
   // CSR-3 block size from the mean rows per super-super-row (sizing on the
   // 90th percentile doubled C3's waves for a 7-12 % loss, r01_ab_csr3_tasks)
   const double ssr_rows = s.mean_rows_per_ssr;
-  s.plan = plan_launch(s.A, dtype, flags, ssr_rows, s.h_rp.data());
+  s.plan = plan_launch(s.A, dtype, flags, ssr_rows,
+                       s.h_tasks.empty() ? 0 : (int64_t)s.h_tasks.size() - 1);
   int rc = build_plan_tables(s, dtype, flags);
   if (rc) return rc;
   s.x = s.d_x;
@@ -504,8 +573,8 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
     if ((rc = validate_host_csr(&view, false)) != HSPMV_OK) return rc;
     s.A.m = (int32_t)A->m; s.A.n = A->n; s.A.nnz = A->nnz;
     s.A.row_ptr = A->row_ptr; s.A.col_idx = A->col_idx; s.A.val = A->val;
+    std::vector<int32_t> cols((size_t)A->nnz);  // host copy until the row tables are built
     {
-      std::vector<int32_t> cols((size_t)A->nnz);
       if (A->nnz)
         HIP_TRY(hipMemcpy(cols.data(), A->col_idx, 4 * (size_t)A->nnz, hipMemcpyDeviceToHost));
       for (int32_t c : cols)
@@ -513,7 +582,6 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
       s.x_entries = count_distinct_cols(cols.data(), A->nnz, A->n);
       bool c16 = false;
       if ((rc = build_col16(s, cols.data(), A->nnz, A->m, A->n, A->dtype, flags, &c16))) return rc;
-      build_xwin(s, rp.data(), cols.data(), A->m);
     }
     if (maps && maps->n_ssr > 0) {
       std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
@@ -528,6 +596,8 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
       s.mean_rows_per_ssr = (double)A->m / (double)maps->n_ssr;
       h->n_ssr = maps->n_ssr; h->n_sr = maps->n_sr;
     }
+    build_row_tables(s, rp.data(), cols.data(), A->m);
+    std::vector<int32_t>().swap(cols);
     const size_t sv = dtype_size(A->dtype);
     if ((rc = dev_alloc(&s.d_x, sv * (size_t)A->n, &s.bytes))) return rc;
     if ((rc = dev_alloc(&s.d_y, sv * (size_t)A->m, &s.bytes))) return rc;
@@ -827,6 +897,7 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->format_bytes = out->alg_bytes;
   for (auto &sh : h->shards) out->format_bytes -= sh.c16_saved;
   out->col16 = s.A.col16 ? 1 + s.A.n_cplanes : 0;
+  out->wave_tasks = s.plan.kernel == kCsr3 ? s.dp.n_tasks : 0;
   return HSPMV_OK;
 }
 

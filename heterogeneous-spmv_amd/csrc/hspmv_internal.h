@@ -40,8 +40,9 @@ constexpr int32_t kLongChunk = 4096;
 // Device-side tables the host planner builds once per shard (all optional).
 struct DevPlan {
   // CSR-3: wave task t covers rows [task_start[t], task_start[t+1]);
+  // either super-rows packed into <= 64-row tasks (default), or
   // waves_per_block tasks per super-super-row, nnz-balanced on super-row
-  // boundaries (the multilevel maps decide the split).
+  // boundaries (HSPMV_CSR3_PLAN=ssr).
   const int32_t *task_start = nullptr;
   int32_t n_tasks = 0;
   // split rows
@@ -71,9 +72,10 @@ struct LaunchPlan {
 };
 
 // Chooses kernel / lanes / block shape for a shard (host-side heuristic).
-// row_ptr_host: the shard's row pointer (m+1) on the host.
+// rows_per_ssr: mean rows per super-super-row (CSR-3 workgroup-per-SSR plan);
+// packed_tasks > 0: CSR-3 tasks packed from super-rows (4 per workgroup).
 LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_per_ssr,
-                       const int32_t *row_ptr_host);
+                       int64_t packed_tasks);
 
 // STREAM / CSR3 row kernels (stream_f32.hip / stream_f64.hip).
 hipError_t launch_rows_f32(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p,

@@ -394,13 +394,14 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
   }
 }
 
-template <typename T, bool NT, int U, bool PF, bool C16, int W>
+template <typename T, bool NT, int U, bool PF, bool C16, int W, bool XW>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, int32_t y_nt,
-    const int32_t *__restrict__ task_start,
+    const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin,
     const int32_t *__restrict__ rp, ColSrc cs, const T *__restrict__ val,
     const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[W * kWave * U];
+  __shared__ T xlds[XW ? W * kXWin : 1];
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t blk = xcd_chunk_remap(blockIdx.x, gridDim.x, xcd_chunk);
@@ -415,7 +416,14 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
   const int32_t r1 = (int32_t)(tb >> 32);
   if (r0 >= r1) return;
   T *my = lds + wid * kWave * U;
-  const XWin<T> nowin{nullptr, 0, 0};
+  XWin<T> win{nullptr, 0, 0};
+  if constexpr (XW) {  // the task's x window (packed tasks: <= 64 rows)
+    const int64_t wv = sload_i64(xwin, (uint64_t)t * 8u);
+    win.lo = (int32_t)wv;
+    win.w = (int32_t)(wv >> 32);
+    win.xs = xlds + wid * kXWin;
+    if (win.w > 0) stage_xwin(xlds + wid * kXWin, x, win.lo, win.w, lane);
+  }
   unsigned long long *ts = nullptr;
 #if (HSPMV_DIAG & 8)
   if (t < kTraceWaves) ts = g_trace + t * kTraceSlots;
@@ -431,8 +439,8 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     const int32_t g1 = min(g0 + kWave, r1);
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
-    wave_rows<T, NT, U, PF, C16, false>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                        nowin, y_nt != 0, ts);
+    wave_rows<T, NT, U, PF, C16, XW>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
+                                     win, y_nt != 0, ts);
     ts = nullptr;
     beg = nbeg;
     end = nend;
@@ -463,15 +471,20 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
                          (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs, xw, val, x, y);
     return;
   }
-#define HSPMV_CSR3(W)                                                                     \
-  hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C16, W>), dim3((unsigned)p.blocks),        \
-                     dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk, \
-                     (int32_t)p.y_nt, dp.task_start, A.row_ptr, cs, val, x, y)
+  const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
+#define HSPMV_CSR3(W, XW)                                                                     \
+  hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C16, W, XW>), dim3((unsigned)p.blocks),        \
+                     dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,     \
+                     (int32_t)p.y_nt, dp.task_start, xw, A.row_ptr, cs, val, x, y)
+  if (xw && p.waves_per_block == 4) {  // x windows: packed tasks only (4 per block)
+    HSPMV_CSR3(4, true);
+    return;
+  }
   switch (p.waves_per_block) {
-    case 1: HSPMV_CSR3(1); break;
-    case 2: HSPMV_CSR3(2); break;
-    case 4: HSPMV_CSR3(4); break;
-    default: HSPMV_CSR3(8); break;
+    case 1: HSPMV_CSR3(1, false); break;
+    case 2: HSPMV_CSR3(2, false); break;
+    case 4: HSPMV_CSR3(4, false); break;
+    default: HSPMV_CSR3(8, false); break;
   }
 #undef HSPMV_CSR3
 }

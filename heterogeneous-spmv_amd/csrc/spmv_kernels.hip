@@ -198,8 +198,7 @@ int pick_u(double nnz_per_pass, int dtype) {
 }  // namespace
 
 LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_per_ssr,
-                       const int32_t *rp_host) {
-  (void)rp_host;
+                       int64_t packed_tasks) {
   LaunchPlan p;
   const unsigned k = flags & 0xFu;
   p.nontemporal = (flags & (1u << 12)) != 0;  // HSPMV_FLAG_NONTEMPORAL
@@ -254,6 +253,14 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
     }
     case kCsr3: {
       p.lanes = kWave;
+      if (packed_tasks > 0) {  // super-rows packed into <= 64-row tasks, 4 per block
+        p.waves_per_block = 4;
+        const double rows_per_task = (double)A.m / (double)packed_tasks;
+        const double per_pass = (rows_per_task < 64.0 ? rows_per_task : 64.0) * d;
+        p.u = forced_u ? forced_u : pick_u(per_pass < 64.0 * kLongRow ? per_pass : 64.0 * kLongRow, dtype);
+        p.blocks = (packed_tasks + 3) / 4;
+        break;
+      }
       // ~64 rows per wave (one lane per row in the ordered sums)
       const double w = rows_per_ssr / 64.0;
       p.waves_per_block = w >= 6.0 ? 8 : (w >= 3.0 ? 4 : (w >= 1.5 ? 2 : 1));

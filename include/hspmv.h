@@ -122,7 +122,7 @@ typedef struct {
                           (< alg_bytes with 16-bit column offsets)          */
   int32_t col16;      /* 0 = 32-bit columns; 1 + p = 16-bit column offsets
                          plus p high-bit planes (see HSPMV_FLAG_NO_COL16)   */
-  int32_t pad_;
+  int32_t wave_tasks; /* CSR3: wave tasks of the launch (GPU 0); 0 otherwise */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
@@ -132,8 +132,9 @@ typedef struct hspmv_handle hspmv_handle;
 #define HSPMV_KERNEL_VECTOR 1u /* L lanes (sub-wave) per row, shuffle sum  */
 #define HSPMV_KERNEL_STREAM 2u /* wave per 64-row group, LDS-staged,
                                   ordered per-row sums (bit-exact vs CPU)  */
-#define HSPMV_KERNEL_CSR3 3u   /* workgroup per super-super-row, waves
-                                  balanced over super-rows by nnz         */
+#define HSPMV_KERNEL_CSR3 3u   /* super-rows packed into <= 64-row wave
+                                  tasks, 4 per workgroup (or one workgroup
+                                  per super-super-row: HSPMV_CSR3_PLAN=ssr) */
 #define HSPMV_KERNEL_MASK 0xFu
 /* lanes per row for VECTOR: HSPMV_LANES(L), L in {1,2,4,8,16,32,64}; 0=auto */
 #define HSPMV_LANES_SHIFT 4

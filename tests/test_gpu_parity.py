@@ -98,16 +98,28 @@ def test_golden_csr3_fixtures(manifest):
                 check_fp64(A, x, y)
 
 
-@pytest.mark.parametrize("waves_case", [(7, 8), (20, 10), (64, 4), (1, 1), (400, 2)])
-def test_csr3_map_sizes(waves_case):
+@pytest.mark.parametrize("plan", ["packed", "ssr"])
+@pytest.mark.parametrize("waves_case", [(7, 8), (20, 10), (64, 4), (1, 1), (400, 2), (2, 100)])
+def test_csr3_map_sizes(waves_case, plan, monkeypatch):
     """Any map granularity (tiny super-rows, one-row super-rows, huge SSRs
-    that need several waves and several 64-row groups) gives the same y."""
+    that need several waves and several 64-row groups, super-rows of more
+    than 64 rows) gives the same y, under both CSR-3 task plans."""
+    if plan == "ssr":
+        monkeypatch.setenv("HSPMV_CSR3_PLAN", "ssr")
     ssrs, srs = waves_case
-    for A in (gen.laplace2d(300, 200), gen.powerlaw(30000, seed=11, dtype=np.float64)):
+    # the banded matrix's tasks take the LDS x-window path (span <= 256 columns)
+    for A in (gen.laplace2d(300, 200), gen.powerlaw(30000, seed=11, dtype=np.float64),
+              gen.banded(20000, per_row=10, half=32, seed=3, dtype=np.float64)):
         maps = hspmv.build_csr3_maps(A, ssrs, srs)
         x = gen.rand_x(A.n, 5)
         y, info = gpu_spmv(A, x, maps)
         assert info["kernel_name"] == "csr3"
+        if plan == "packed":  # whole super-rows per task, <= 64 rows each
+            sr_rows = np.diff(maps.inner)
+            lower = int(np.ceil(A.m / 64))
+            assert lower <= info["wave_tasks"] <= len(sr_rows) + int(np.sum(sr_rows // 64)) + 1
+        else:
+            assert info["wave_tasks"] == maps.n_ssr * info["waves_per_block"]
         check_fp64(A, x, y, exact_rows=short_rows(A))
 
 
