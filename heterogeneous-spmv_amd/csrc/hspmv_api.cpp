@@ -276,36 +276,48 @@ void pack_csr3_tasks(Shard &s) {
 }
 
 // x windows of row groups [starts[g], starts[g+1]) -- the 64-row groups of
-// STREAM when starts is null, the packed CSR-3 tasks otherwise: {lo, w} when
-// the group's columns span w <= kXWin entries, else {0, 0}.  Empty when
-// fewer than half the groups fit (HSPMV_XWIN=0 disables).
+// STREAM when starts is null, the packed CSR-3 tasks otherwise: {lo, w}
+// when the group's columns span w <= kXWin entries, else {0, 0}.  Empty
+// when fewer than half the groups fit (HSPMV_XWIN=0 disables).  Several
+// windows per group (C2's Laplacian: three runs around r-1000, r, r+1000)
+// were measured and dropped: 15.6 -> 17.2 us on C2, 210 -> 232 us on a
+// 4000^2 Laplacian (profiles/r01_ab_xwin_multi.jsonl) -- the staging and
+// its registers cost more than gathers that hit L2.
 std::vector<int32_t> xwin_table(const int32_t *rp, const int32_t *col, int64_t m,
                                 const std::vector<int32_t> *starts) {
-  std::vector<int32_t> w;
+  std::vector<int32_t> tab;
   if (const char *e = getenv("HSPMV_XWIN"))
-    if (atoi(e) == 0) return w;
+    if (atoi(e) == 0) return tab;
   const int64_t ng = starts ? (int64_t)starts->size() - 1 : (m + 63) / 64;
-  if (ng <= 0) return w;
-  w.assign((size_t)(2 * ng), 0);
-  int64_t fit = 0;
-  for (int64_t g = 0; g < ng; ++g) {
-    const int64_t r0 = starts ? (*starts)[(size_t)g] : 64 * g;
-    const int64_t r1 = starts ? (*starts)[(size_t)g + 1] : std::min(m, 64 * g + 64);
-    const int64_t k0 = rp[r0], k1 = rp[r1];
-    if (k1 <= k0) continue;
-    int32_t lo = col[k0], hi = col[k0];
-    for (int64_t k = k0 + 1; k < k1; ++k) {
-      lo = std::min(lo, col[k]);
-      hi = std::max(hi, col[k]);
-    }
-    if ((int64_t)hi - lo + 1 <= kXWin) {
-      w[(size_t)(2 * g)] = lo;
-      w[(size_t)(2 * g + 1)] = hi - lo + 1;
-      ++fit;
-    }
-  }
-  if (2 * fit < ng) w.clear();
-  return w;
+  if (ng <= 0) return tab;
+  tab.assign((size_t)(2 * ng), 0);
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, ng / 4096));
+  std::vector<int64_t> fit((size_t)nt, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t]() {
+      for (int64_t g = ng * t / nt; g < ng * (t + 1) / nt; ++g) {
+        const int64_t r0 = starts ? (*starts)[(size_t)g] : 64 * g;
+        const int64_t r1 = starts ? (*starts)[(size_t)g + 1] : std::min(m, 64 * g + 64);
+        const int64_t k0 = rp[r0], k1 = rp[r1];
+        if (k1 <= k0) continue;
+        int32_t lo = col[k0], hi = col[k0];
+        for (int64_t k = k0 + 1; k < k1; ++k) {
+          lo = std::min(lo, col[k]);
+          hi = std::max(hi, col[k]);
+        }
+        if ((int64_t)hi - lo + 1 <= kXWin) {
+          tab[(size_t)(2 * g)] = lo;
+          tab[(size_t)(2 * g + 1)] = hi - lo + 1;
+          ++fit[(size_t)t];
+        }
+      }
+    });
+  for (auto &x : th) x.join();
+  int64_t nfit = 0;
+  for (int64_t f : fit) nfit += f;
+  if (2 * nfit < ng) tab.clear();
+  return tab;
 }
 
 // Host-side tables that need the columns (built at upload, while they are
@@ -314,7 +326,8 @@ void build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, int64_t m
   s.h_tasks.clear();
   if (s.A.n_ssr > 0 && csr3_packed()) pack_csr3_tasks(s);
   s.h_xwin = xwin_table(rp, col, m, nullptr);
-  s.h_xwin_t = s.h_tasks.empty() ? std::vector<int32_t>() : xwin_table(rp, col, m, &s.h_tasks);
+  s.h_xwin_t.clear();
+  if (!s.h_tasks.empty()) s.h_xwin_t = xwin_table(rp, col, m, &s.h_tasks);
 }
 
 // Uploads rows [r0, r1) of A (and the matching slice of the maps) to shard s.
@@ -898,6 +911,7 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   for (auto &sh : h->shards) out->format_bytes -= sh.c16_saved;
   out->col16 = s.A.col16 ? 1 + s.A.n_cplanes : 0;
   out->wave_tasks = s.plan.kernel == kCsr3 ? s.dp.n_tasks : 0;
+  out->x_windows = s.dp.xwin ? 1 : 0;
   return HSPMV_OK;
 }
 

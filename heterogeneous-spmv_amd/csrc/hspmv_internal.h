@@ -27,7 +27,7 @@ struct DevCSR {
 };
 
 constexpr int kC16Shift = 8;  // 256 nonzeros per column-base block
-constexpr int kXWin = 256;    // largest LDS-staged x window of a STREAM group (entries)
+constexpr int kXWin = 256;    // largest LDS-staged x window of a row group (entries)
 
 enum Kernel : int { kAuto = 0, kVector = 1, kStream = 2, kCsr3 = 3 };
 
@@ -52,8 +52,9 @@ struct DevPlan {
   const int32_t *long_cstart = nullptr; // n_long+1, chunk ranges per split row
   const int32_t *chunk_k = nullptr;     // 2*n_chunks: [k0, k1) per chunk
   void *partials = nullptr;             // n_chunks partial sums (dtype)
-  // STREAM x windows: per 64-row group {lo, w}, w = 0 when the group's
-  // columns span more than kXWin entries (then it gathers from global x)
+  // x windows per row group (STREAM: 64-row groups; CSR3: packed tasks):
+  // {lo, w} (int32), w = 0 when the group's columns span more than kXWin
+  // entries (then it gathers from global x)
   const void *xwin = nullptr;
 };
 

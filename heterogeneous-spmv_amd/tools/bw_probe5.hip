@@ -1,0 +1,138 @@
+// bw_probe5.hip -- calibration microbenchmark (not product code): what a
+// launch that reads C2's bytes from the Infinity Cache can cost at best.
+// Back-to-back launches (the bench.py protocol: events around K launches),
+// Infinity-Cache-resident buffers, for
+//   empty   : the C2 STREAM grid (3907 x 256) doing nothing
+//   read B  : B bytes read once, 16 B per lane, one segment per wave
+//   read+w  : the same plus 8 MB of stores (C2's y)
+// at B = 20 .. 160 MB, and the same grids with 1 block per CU-slot loop
+// (persistent: 256 x 8 blocks, grid-stride).
+//
+//   hipcc -O3 --offload-arch=gfx950 bw_probe5.hip -o bw_probe5 && ./bw_probe5
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+typedef double dv2 __attribute__((ext_vector_type(2)));  // 16 B per lane
+
+#define CK(x)                                                                       \
+  do {                                                                              \
+    hipError_t e = (x);                                                             \
+    if (e != hipSuccess) {                                                          \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                        \
+      return 1;                                                                     \
+    }                                                                               \
+  } while (0)
+
+__global__ __launch_bounds__(256) void empty_k(double *out) {
+  if (threadIdx.x == 1000) out[0] = 1.0;
+}
+
+// each wave reads `per_wave` 16-B vectors (contiguous), optional store of
+// one double per lane of the first `store_lanes` lanes-worth
+__global__ __launch_bounds__(256) void read_k(const dv2 *__restrict__ in, long n_vec,
+                                              int per_wave, double *__restrict__ y, long n_y,
+                                              double *out) {
+  const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const long v0 = w * per_wave;
+  double s = 0.0;
+  for (int i = lane; i < per_wave; i += 64) {
+    const long v = v0 + i;
+    if (v < n_vec) {
+      const dv2 t = __builtin_nontemporal_load(in + v);
+      s += t.x + t.y;
+    }
+  }
+  if (n_y) {
+    const long r = w * 64 + lane;
+    if (r < n_y) y[r] = s;
+  } else if (s == 12345.678) {
+    out[0] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void read_plain_k(const dv2 *__restrict__ in, long n_vec,
+                                                    int per_wave, double *__restrict__ y, long n_y,
+                                                    double *out) {
+  const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const long v0 = w * per_wave;
+  double s = 0.0;
+  for (int i = lane; i < per_wave; i += 64) {
+    const long v = v0 + i;
+    if (v < n_vec) {
+      const dv2 t = in[v];
+      s += t.x + t.y;
+    }
+  }
+  if (n_y) {
+    const long r = w * 64 + lane;
+    if (r < n_y) y[r] = s;
+  } else if (s == 12345.678) {
+    out[0] = s;
+  }
+}
+
+template <typename F>
+float per_launch_us(F launch, int k) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  for (int i = 0; i < 20; ++i) launch();
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {
+    (void)hipEventRecord(a);
+    for (int i = 0; i < k; ++i) launch();
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    if (ms < best) best = ms;
+  }
+  return best * 1000.0f / k;
+}
+
+int main() {
+  const long max_bytes = 160L << 20;
+  dv2 *in;
+  double *y, *out;
+  CK(hipMalloc(&in, max_bytes));
+  CK(hipMalloc(&y, 8L << 20));
+  CK(hipMalloc(&out, 64));
+  CK(hipMemset(in, 0, max_bytes));
+  CK(hipMemset(y, 0, 8L << 20));
+  const int K = 200;
+  {
+    const unsigned grid = 3907;  // C2: 1M rows / 64 per wave / 4 waves
+    const float us = per_launch_us([&] { hipLaunchKernelGGL(empty_k, dim3(grid), dim3(256), 0, 0, out); }, K);
+    printf("{\"variant\": \"empty\", \"grid\": %u, \"us\": %.3f}\n", grid, us);
+  }
+  for (long mb : {20L, 40L, 60L, 80L, 120L, 160L}) {
+    const long bytes = mb * 1000000L;
+    const long n_vec = bytes / 16;
+    for (int waves_c2 : {1, 0}) {
+      // waves_c2: the C2 grid (15625 waves), else 8 waves per SIMD x 1024 SIMDs
+      const long waves = waves_c2 ? 15625 : 256L * 4 * 8;
+      const int per_wave = (int)((n_vec + waves - 1) / waves);
+      const unsigned grid = (unsigned)((waves + 3) / 4);
+      for (int st : {0, 1}) {
+        const long n_y = st ? 1000000 : 0;
+        const float us_nt = per_launch_us([&] {
+          hipLaunchKernelGGL(read_k, dim3(grid), dim3(256), 0, 0, in, n_vec, per_wave, y, n_y, out);
+        }, K);
+        const float us = per_launch_us([&] {
+          hipLaunchKernelGGL(read_plain_k, dim3(grid), dim3(256), 0, 0, in, n_vec, per_wave, y, n_y, out);
+        }, K);
+        const double tot = (double)bytes + (st ? 8e6 : 0.0);
+        printf("{\"variant\": \"read%s\", \"MB\": %ld, \"grid\": %u, \"us_plain\": %.3f, \"GBps_plain\": %.0f, "
+               "\"us_nt\": %.3f, \"GBps_nt\": %.0f}\n",
+               st ? "+y" : "", mb, grid, us, tot / us * 1e-3, us_nt, tot / us_nt * 1e-3);
+        fflush(stdout);
+      }
+    }
+  }
+  CK(hipGetLastError());
+  return 0;
+}

@@ -72,6 +72,9 @@ def build(cfg):
     if cfg == "s27n":  # diagnostic: C3's stencil in natural (non-RCM) order
         A = gen.stencil27(125, rcm=False)
         return A, None, "diag: 27-pt 125^3 natural order fp64"
+    if cfg == "l4k":  # diagnostic: HBM-resident 5-pt Laplacian (three x windows per group)
+        A = gen.laplace2d(4000, 4000)
+        return A, None, "diag: 5-pt Laplacian 4000^2 CSR fp64 (HBM-resident)"
     if cfg == "c5":
         A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32)
         maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))

@@ -123,6 +123,10 @@ typedef struct {
   int32_t col16;      /* 0 = 32-bit columns; 1 + p = 16-bit column offsets
                          plus p high-bit planes (see HSPMV_FLAG_NO_COL16)   */
   int32_t wave_tasks; /* CSR3: wave tasks of the launch (GPU 0); 0 otherwise */
+  int32_t x_windows;  /* STREAM/CSR3: 1 = row groups whose columns span
+                         <= 256 entries gather from an LDS copy of that x
+                         window; 0 = every gather from global x (GPU 0)     */
+  int32_t pad_;
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;

@@ -123,6 +123,28 @@ def test_csr3_map_sizes(waves_case, plan, monkeypatch):
         check_fp64(A, x, y, exact_rows=short_rows(A))
 
 
+@pytest.mark.parametrize("xwin", ["0", "1"])
+def test_x_window_variants_identical(xwin, monkeypatch):
+    """Global gathers and LDS x windows give the same bits (the windows only
+    change where x[col] is read from), for STREAM and for packed CSR-3
+    tasks; groups whose columns do not fit a window mix in."""
+    if xwin == "0":
+        monkeypatch.setenv("HSPMV_XWIN", "0")
+    rng = np.random.default_rng(4)
+    A0 = gen.banded(40000, per_row=10, half=32, seed=6)
+    # every 7th group gets a far column, so some groups do not fit
+    ci = A0.col_idx.copy()
+    far = np.arange(0, A0.m, 64 * 7)
+    ci[A0.row_ptr[far]] = rng.integers(0, A0.n, far.size)
+    A = hspmv.CsrMatrix(A0.m, A0.n, A0.row_ptr, ci, A0.val)
+    x = gen.rand_x(A.n, 12)
+    maps = hspmv.build_csr3_maps(A, 7, 8)
+    for mp in (None, maps):
+        y, info = gpu_spmv(A, x, mp)
+        assert info["x_windows"] == int(xwin)
+        check_fp64(A, x, y, exact_rows=slice(None))
+
+
 def test_nontemporal_variants_identical():
     A = gen.stencil27(20)
     x = gen.rand_x(A.n, 8)
@@ -206,6 +228,8 @@ def test_config_c2_laplacian_1m_fp64():
         for kernel in ("auto", "vector"):
             y, info = gpu_spmv(A, x, kernel=kernel)
             check_fp64(A, x, y, exact_rows=slice(None) if kernel == "auto" else None)
+            if kernel == "auto":  # Infinity-Cache resident: gathers, no x windows
+                assert info["x_windows"] == 0
 
 
 def test_config_c3_stencil27_csr3_fp64():
@@ -227,8 +251,9 @@ def test_config_c4_banded_shard_fp64():
     splits = np.linspace(0, m, 9).astype(np.int64)
     A = gen.banded(m, r0=int(splits[3]), r1=int(splits[4]))
     x = gen.rand_x(m, 11)
-    y, _ = gpu_spmv(A, x)
+    y, info = gpu_spmv(A, x)
     check_fp64(A, x, y, exact_rows=slice(None))
+    assert info["x_windows"] == 1  # one window of <= 128 columns per group
 
 
 def test_config_c5_powerlaw_csr3_fp32():
