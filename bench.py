@@ -18,7 +18,10 @@ Extra fields on the line:
                average launch duration on the launch stream, vs 8 TB/s HBM
   cold         the same SpMV with the 256 MiB Infinity Cache flushed before
                every launch (the C2 matrix, 80 MB, is MALL-resident when warm)
-  comm         RCCL x broadcast / y all-gather times (N > 1), timed separately
+  comm         RCCL x broadcast / y all-gather / halo-exchange times (N > 1),
+               timed separately, and the end-to-end rates they imply:
+               2 nnz / (step + y all-gather), and the iterative form
+               2 nnz / (step + halo exchange) where x is distributed like y
   cpu_baseline the oracle's OpenMP restatement of spmv-csr's omp_spmv on the
                host cores, rank 0 at N = 1 only (bounded sample)
 """
@@ -123,17 +126,26 @@ def cpu_baseline(A, x, budget_s: float):
     import oracle  # test infrastructure: the CPU baseline leg only
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     threads = min(threads, os.cpu_count() or threads)
-    oracle.set_schedule("static", threads)
-    tmin, tmax, tavg, used = oracle.time_spmv(A.row_ptr, A.col_idx, A.val, x, warmup=5, runs=20)
-    runs = int(max(20, min(20000, budget_s / max(tavg, 1e-6))))
-    tmin, tmax, tavg, used = oracle.time_spmv(A.row_ptr, A.col_idx, A.val, x, warmup=5, runs=runs)
-    return {"value": round(2.0 * A.nnz / tavg * 1e-9, 3), "unit": "GFLOP/s", "cores": int(used),
+    res = {}
+    for sched in ("static", "guided"):  # run_norm.py:18,66 / run_cuda_new.py:79
+        oracle.set_schedule(sched, threads)
+        tmin, tmax, tavg, used = oracle.time_spmv(A.row_ptr, A.col_idx, A.val, x, warmup=5, runs=20)
+        runs = int(max(20, min(20000, budget_s / max(tavg, 1e-6))))
+        tmin, tmax, tavg, used = oracle.time_spmv(A.row_ptr, A.col_idx, A.val, x, warmup=5,
+                                                  runs=runs)
+        res[sched] = (tmin, tmax, tavg, int(used), runs)
+    tmin, tmax, tavg, used, runs = res["static"]
+    g = res["guided"]
+    return {"value": round(2.0 * A.nnz / tavg * 1e-9, 3), "unit": "GFLOP/s", "cores": used,
             "kind": "port",
             "sample": (f"full C2 matrix (m={A.m}, nnz={A.nnz}) fp64, omp_spmv restatement "
                        f"(oracle/spmv_oracle.c), OMP_SCHEDULE=static, 5 warm-ups + {runs} timed "
                        f"runs (spmv-csr/spmv.c:164-185 protocol), value from TimeAvg"),
             "time_min_s": tmin, "time_avg_s": tavg, "time_max_s": tmax,
-            "gflops_from_min": round(2.0 * A.nnz / tmin * 1e-9, 3)}
+            "gflops_from_min": round(2.0 * A.nnz / tmin * 1e-9, 3),
+            "guided": {"gflops": round(2.0 * A.nnz / g[2] * 1e-9, 3),
+                       "gflops_from_min": round(2.0 * A.nnz / g[0] * 1e-9, 3),
+                       "time_avg_s": g[2], "runs": g[4]}}
 
 
 def main():
@@ -205,15 +217,35 @@ def main():
     ok, rel = hdist.checksum_ok(A, x.cpu().numpy(), y_host)
     ok_all = sum_over_ranks(1.0 if ok else 0.0, world) == world
 
-    # exchange step costs (reported, not in the step): y all-gather over RCCL
-    gather_ms = None
+    # exchange step costs (reported, not in the step): y all-gather over RCCL,
+    # and the halo exchange that replaces the x broadcast when x is
+    # distributed like y (iterative use; point-to-point RCCL send/recv)
+    gather_ms = halo_ms = None
+    halo_b = 0
     if world > 1:
-        barrier(world)
-        t0 = time.perf_counter()
-        yfull = hdist.gather_y(y, shard.splits)
-        barrier(world)
-        gather_ms = (time.perf_counter() - t0) * 1e3
-        del yfull
+        times = []
+        for _ in range(5):
+            barrier(world)
+            t0 = time.perf_counter()
+            yfull = hdist.gather_y(y, shard.splits)
+            barrier(world)
+            times.append((time.perf_counter() - t0) * 1e3)
+            del yfull
+        gather_ms = max_over_ranks(float(np.median(times)), world)
+        halo = hdist.plan_halo(A, shard.splits, rank, world)
+        xw = x[halo.lo:halo.hi].clone()
+        times = []
+        for _ in range(20):
+            barrier(world)
+            t0 = time.perf_counter()
+            hdist.halo_exchange(xw, halo)
+            torch.cuda.synchronize()
+            times.append((time.perf_counter() - t0) * 1e3)
+        halo_ms = max_over_ranks(float(np.median(times)), world)
+        halo_b = int(max_over_ranks(float(hdist.halo_bytes(halo)), world))
+        halo_ok = bool(torch.equal(xw, x[halo.lo:halo.hi]))
+        ok_all = ok_all and sum_over_ranks(1.0 if halo_ok else 0.0, world) == world
+        del xw
 
     flops_step = 2.0 * shard.nnz_global
     alg_local = info["alg_bytes"]  # x counted as the distinct columns this shard reads
@@ -261,7 +293,13 @@ def main():
                      "note": "a 512 MiB read before each launch evicts the Infinity Cache"},
             "comm": {"bcast_x_ms": round(bcast_ms, 3) if world > 1 else None,
                      "gather_y_ms": round(gather_ms, 3) if gather_ms is not None else None,
-                     "x_bytes": shard.n_global * 8, "y_bytes": shard.m_global * 8},
+                     "halo_x_ms": round(halo_ms, 4) if halo_ms is not None else None,
+                     "x_bytes": shard.n_global * 8, "y_bytes": shard.m_global * 8,
+                     "halo_bytes_per_rank": halo_b if world > 1 else None,
+                     "end_to_end_gflops": (round(flops_step / (step_s + gather_ms * 1e-3) * 1e-9, 3)
+                                           if gather_ms is not None else round(gflops, 3)),
+                     "iterative_gflops": (round(flops_step / (step_s + halo_ms * 1e-3) * 1e-9, 3)
+                                          if halo_ms is not None else round(gflops, 3))},
             "check": {"pass": bool(ok_all), "checksum_rel": rel},
             "cpu_baseline": cpu,
         }

@@ -10,6 +10,15 @@ indices, and needs the whole x.  The two exchange steps of the path are
   * y gather into a full-length vector (``gather_y``): an all-gather of the
     shards padded to the longest one, then unpadded.
 
+For iterative use on banded / mesh matrices (C2's Laplacian, C4's band) x is
+distributed like y -- rank r owns x[splits[r]:splits[r+1]] -- and the x
+broadcast is replaced by a halo exchange (SURVEY.md §8e "banded optional
+mode"): each rank keeps only the x window [lo, hi) its rows reference
+(``localize``), and receives the parts of it other ranks own by point-to-point
+send/recv (``plan_halo`` / ``halo_exchange``; RCCL ncclSend/ncclRecv under
+the "nccl" backend).  At C4 that is 2 x 32 entries per neighbour instead of
+the 160 MB x.
+
 Both go through ``torch.distributed`` (backend "nccl" = RCCL over xGMI on the
 GPU box, "gloo" on the CPU in tests).  Workloads are built per rank from the
 seeded generators in :mod:`hspmv.gen`, so no rank ever materialises the global
@@ -129,3 +138,77 @@ def checksum_ok(A: CsrMatrix, x: np.ndarray, y: np.ndarray, seed: int = 99) -> t
     rel = abs(lhs - rhs) / scale
     tol = 1e-12 if A.val.dtype == np.float64 else 1e-5
     return rel <= tol, rel
+
+
+# ------------------------------------------------------------------ halo mode
+
+@dataclass
+class Halo:
+    lo: int               # this rank's x window is x[lo:hi)
+    hi: int
+    own: tuple            # x[own[0]:own[1]] is owned (computed) by this rank
+    recvs: list           # (peer, g0, g1): receive x[g0:g1] from peer
+    sends: list           # (peer, g0, g1): send x[g0:g1] to peer
+
+
+def column_window(A: CsrMatrix, own: tuple) -> tuple:
+    """[lo, hi): the smallest x range holding every column of A and the
+    rank's own entries."""
+    lo, hi = int(own[0]), int(own[1])
+    if A.nnz:
+        lo = min(lo, int(A.col_idx.min()))
+        hi = max(hi, int(A.col_idx.max()) + 1)
+    return lo, hi
+
+
+def localize(A: CsrMatrix, lo: int, hi: int) -> CsrMatrix:
+    """A with columns rebased to its x window [lo, hi) (n = hi - lo)."""
+    return CsrMatrix(A.m, hi - lo, A.row_ptr, (A.col_idx - lo).astype(np.int32), A.val)
+
+
+def plan_halo(A: CsrMatrix, splits: np.ndarray, rank: int, world: int) -> Halo:
+    """Who sends which part of x to whom.  x is distributed like the rows
+    (square matrix); one all-gather of the (lo, hi) windows, then every rank
+    intersects the windows with the owned ranges."""
+    import torch
+    import torch.distributed as dist
+    own = (int(splits[rank]), int(splits[rank + 1]))
+    lo, hi = column_window(A, own)
+    win = torch.tensor([lo, hi], dtype=torch.int64)
+    if dist.get_backend() == "nccl":
+        win = win.cuda()
+    allw = [torch.empty_like(win) for _ in range(world)]
+    dist.all_gather(allw, win)
+    allw = [tuple(int(v) for v in w.cpu()) for w in allw]
+    recvs, sends = [], []
+    for q in range(world):
+        if q == rank:
+            continue
+        q0, q1 = int(splits[q]), int(splits[q + 1])
+        g0, g1 = max(lo, q0), min(hi, q1)          # of my window, owned by q
+        if g1 > g0:
+            recvs.append((q, g0, g1))
+        w0, w1 = allw[q]
+        g0, g1 = max(w0, own[0]), min(w1, own[1])  # of q's window, owned by me
+        if g1 > g0:
+            sends.append((q, g0, g1))
+    return Halo(lo, hi, own, recvs, sends)
+
+
+def halo_exchange(x_win, halo: Halo) -> None:
+    """Fills the non-owned parts of x_win (a torch tensor holding x[lo:hi),
+    own part already written) from the ranks that own them."""
+    import torch.distributed as dist
+    ops = []
+    for q, g0, g1 in halo.sends:
+        ops.append(dist.P2POp(dist.isend, x_win[g0 - halo.lo:g1 - halo.lo].contiguous(), q))
+    for q, g0, g1 in halo.recvs:
+        ops.append(dist.P2POp(dist.irecv, x_win[g0 - halo.lo:g1 - halo.lo], q))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+
+def halo_bytes(halo: Halo, itemsize: int = 8) -> int:
+    """Bytes this rank receives per exchange."""
+    return sum(g1 - g0 for _, g0, g1 in halo.recvs) * itemsize
