@@ -55,6 +55,12 @@ struct Shard {
   int32_t *d_cbase = nullptr;
   uint64_t *d_cplanes = nullptr;
   int32_t *d_xwin = nullptr;         // STREAM x windows {lo, w} per 64-row group
+  int32_t *d_xd_blk = nullptr;       // block x dictionaries (build_xdict)
+  int32_t *d_xd_runs = nullptr;
+  int32_t xd_lds_bytes = 0;
+  int xd_shape = 0;                  // 0 none, kStream (256-row blocks), kCsr3 (4 packed tasks)
+  int64_t xd_entries = 0;            // x entries staged per SpMV (all blocks)
+  int64_t xd_runs_n = 0;             // run records incl. sentinels
   std::vector<int32_t> h_xwin;       // built at upload (host columns at hand)
   std::vector<int32_t> h_xwin_t;     // the same per packed CSR-3 task
   void *d_val = nullptr;
@@ -124,6 +130,8 @@ void free_shard(Shard &s, bool borrowed) {
   (void)hipFree(s.d_cbase);
   (void)hipFree(s.d_cplanes);
   (void)hipFree(s.d_xwin);
+  (void)hipFree(s.d_xd_blk);
+  (void)hipFree(s.d_xd_runs);
   (void)hipFree(s.d_task);
   (void)hipFree(s.d_long_row);
   (void)hipFree(s.d_long_cstart);
@@ -246,11 +254,8 @@ bool csr3_packed() {
   return !(e && !strcmp(e, "ssr"));
 }
 
-void pack_csr3_tasks(Shard &s) {
+void pack_csr3_tasks(const std::vector<int32_t> &in, int32_t m, std::vector<int32_t> &ts) {
   constexpr int32_t kTaskRows = 64;  // one wave's lanes
-  const std::vector<int32_t> &in = s.h_inner;
-  const int32_t m = s.A.m;
-  std::vector<int32_t> &ts = s.h_tasks;
   ts.clear();
   ts.reserve((size_t)m / 32 + 2);
   int32_t start = 0;
@@ -320,14 +325,212 @@ std::vector<int32_t> xwin_table(const int32_t *rp, const int32_t *col, int64_t m
   return tab;
 }
 
+// Block x dictionaries.  Per workgroup (STREAM: 256 consecutive rows; CSR3:
+// four consecutive packed tasks) the distinct columns its in-kernel rows
+// reference, as runs of consecutive columns (gaps of <= kXdGap unused
+// entries are bridged, so a run is one contiguous load); the kernel stages
+// them in LDS once per workgroup and every nonzero's column becomes a 16-bit
+// position in that copy.  The gathers (one per nonzero, spread over many L2
+// lines) become contiguous loads plus ds_reads, and the index stream is
+// 2 B/nnz with no bases or planes.  On C3 (27-point RCM stencil) 256 rows
+// reference ~1500 distinct x in ~4 runs, against ~6800 nonzeros.
+// Auto: matrices that stream from HBM, whose largest dictionary fits
+// kXdCapBytes of LDS and whose staged entries are <= half the nonzeros;
+// HSPMV_XDICT=0/1 turns it off / on (on: whenever it fits the cap),
+// HSPMV_XDICT_CAP=<bytes> moves the cap.  Splits rows (> kLongRow) keep
+// their 32-bit columns (split-row kernels).
+constexpr int32_t kXdGap = 8;
+constexpr int32_t kXdMaxRuns = 63;          // run records per block live in one wave's lanes
+constexpr int32_t kXdCapBytes = 20 * 1024;  // + 8-12 KB of product staging: 6 blocks/CU
+
+// Which row kernel the planner will pick (plan_launch) for a shard with
+// n_ssr super-super-rows and (CSR-3) packed tasks.
+int kernel_for_tables(int64_t n_ssr, bool have_tasks, unsigned flags) {
+  const unsigned k = flags & 0xFu;
+  if (k == kVector) return kVector;
+  if ((k == kCsr3 || k == kAuto) && n_ssr > 0)
+    return have_tasks ? kCsr3 : -1;  // workgroup-per-SSR plan: no dictionaries
+  return kStream;
+}
+
+// The dictionaries of the workgroups whose rows are [bs[b], bs[b+1]).
+struct XdPlan {
+  std::vector<int32_t> blk;  // nb + 1 record ranges
+  std::vector<int32_t> rec;  // {x_start, lds_off} per run, sentinel {0, entries} per block
+  std::vector<uint16_t> pos; // per nonzero: position in its block's staged x (0 for split rows)
+  int64_t entries = 0, in_kernel_nnz = 0;
+  int32_t tmax = 0;
+};
+
+// false when some block needs more than cap entries.
+bool plan_xdict(const int32_t *rp, const int32_t *col, const std::vector<int32_t> &bs,
+                int32_t long_t, int64_t cap, bool fill, XdPlan &P) {
+  const int64_t nb = (int64_t)bs.size() - 1;
+  const int64_t nnz = rp[bs.back()];
+  std::vector<std::vector<int32_t>> runs((size_t)nb);  // per block: start, end (inclusive) pairs
+  std::vector<int32_t> total((size_t)nb, 0);
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, nb / 256));
+  std::atomic<bool> fail{false};
+  auto par = [&](auto &&body) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back([&, t]() { body(nb * t / nt, nb * (t + 1) / nt); });
+    for (auto &x : th) x.join();
+  };
+  par([&](int64_t b0, int64_t b1) {
+    std::vector<int32_t> c;
+    for (int64_t b = b0; b < b1 && !fail.load(std::memory_order_relaxed); ++b) {
+      c.clear();
+      for (int32_t r = bs[(size_t)b]; r < bs[(size_t)b + 1]; ++r)
+        if (rp[r + 1] - rp[r] <= long_t) c.insert(c.end(), col + rp[r], col + rp[r + 1]);
+      std::sort(c.begin(), c.end());
+      c.erase(std::unique(c.begin(), c.end()), c.end());
+      std::vector<int32_t> &R = runs[(size_t)b];
+      for (int64_t gap = kXdGap;; gap *= 2) {  // bridge wider gaps until the runs fit a wave
+        R.clear();
+        for (int32_t v : c) {
+          if (!R.empty() && (int64_t)v - R.back() <= gap) {
+            R.back() = v;
+          } else {
+            R.push_back(v);
+            R.push_back(v);
+          }
+        }
+        if ((int64_t)R.size() / 2 <= kXdMaxRuns) break;
+      }
+      int64_t tot = 0;
+      for (size_t i = 0; i < R.size(); i += 2) tot += (int64_t)R[i + 1] - R[i] + 1;
+      if (tot > cap) fail = true;
+      total[(size_t)b] = (int32_t)std::min<int64_t>(tot, INT32_MAX);
+    }
+  });
+  if (fail) return false;
+  int64_t nrec = 0;
+  P.blk.assign((size_t)nb + 1, 0);
+  P.entries = 0;
+  P.tmax = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    P.entries += total[(size_t)b];
+    P.tmax = std::max(P.tmax, total[(size_t)b]);
+    P.blk[(size_t)b] = (int32_t)nrec;
+    nrec += (int64_t)runs[(size_t)b].size() / 2 + 1;
+  }
+  P.blk[(size_t)nb] = (int32_t)nrec;
+  P.in_kernel_nnz = 0;
+  for (int32_t r = bs.front(); r < bs.back(); ++r)
+    if (rp[r + 1] - rp[r] <= long_t) P.in_kernel_nnz += rp[r + 1] - rp[r];
+  if (!fill) return true;
+  P.rec.assign((size_t)(2 * nrec), 0);
+  P.pos.assign((size_t)nnz, 0);
+  par([&](int64_t b0, int64_t b1) {
+    for (int64_t b = b0; b < b1; ++b) {
+      const std::vector<int32_t> &R = runs[(size_t)b];
+      const int64_t nr = (int64_t)R.size() / 2;
+      int32_t *o = P.rec.data() + 2 * (size_t)P.blk[(size_t)b];
+      int32_t off = 0;
+      for (int64_t i = 0; i < nr; ++i) {
+        o[2 * i] = R[2 * i];
+        o[2 * i + 1] = off;
+        off += R[2 * i + 1] - R[2 * i] + 1;
+      }
+      o[2 * nr] = 0;
+      o[2 * nr + 1] = off;  // sentinel: entries of the block
+      for (int32_t r = bs[(size_t)b]; r < bs[(size_t)b + 1]; ++r) {
+        if (rp[r + 1] - rp[r] > long_t) continue;
+        for (int32_t k = rp[r]; k < rp[r + 1]; ++k) {
+          // last run starting at or before col[k] (runs sorted by start)
+          int64_t lo = 0, hi = nr - 1;
+          while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) / 2;
+            if (R[2 * mid] <= col[k]) lo = mid; else hi = mid - 1;
+          }
+          P.pos[(size_t)k] = (uint16_t)(o[2 * lo + 1] + (col[k] - R[2 * lo]));
+        }
+      }
+    }
+  });
+  return true;
+}
+
+// Workgroup row ranges of the row kernel `kern` (STREAM: 256 rows; CSR3:
+// four packed tasks).
+std::vector<int32_t> xdict_blocks(int kern, int64_t m, const std::vector<int32_t> &tasks) {
+  std::vector<int32_t> bs;
+  if (kern == kStream) {
+    for (int64_t r = 0; r < m; r += 256) bs.push_back((int32_t)r);
+    bs.push_back((int32_t)m);
+  } else {
+    const int64_t nt = (int64_t)tasks.size() - 1;
+    for (int64_t t = 0; t < nt; t += 4) bs.push_back(tasks[(size_t)t]);
+    bs.push_back(tasks[(size_t)nt]);
+  }
+  return bs;
+}
+
+int64_t xdict_cap_entries(int dtype) {
+  int64_t cap_bytes = kXdCapBytes;
+  if (const char *e = getenv("HSPMV_XDICT_CAP")) cap_bytes = atoll(e);
+  // <= 64 KiB of LDS (and 16-bit positions) whatever HSPMV_XDICT_CAP asks
+  return std::min<int64_t>(std::min<int64_t>(cap_bytes, 64 * 1024) / (int64_t)dtype_size(dtype),
+                           65536);
+}
+
+int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int64_t n, int dtype,
+                unsigned flags) {
+  s.xd_shape = 0;
+  const char *env = getenv("HSPMV_XDICT");
+  const int mode = env ? atoi(env) : -1;  // -1 auto, 0 off, 1 on when it fits
+  if (mode == 0 || (flags & HSPMV_FLAG_NO_COL16) || m == 0) return HSPMV_OK;
+  const int kern = kernel_for_tables(s.A.n_ssr, !s.h_tasks.empty(), flags);
+  if (kern != kStream && kern != kCsr3) return HSPMV_OK;
+  if (kern == kStream && ((flags >> 29) & 0x7u) > 1) return HSPMV_OK;  // groups != 1
+  const double sv = (double)dtype_size(dtype);
+  const int64_t nnz = rp[m];
+  const double footprint = (double)nnz * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv;
+  if (mode < 0 && footprint <= kMallResident) return HSPMV_OK;
+  const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
+  XdPlan P;
+  if (!plan_xdict(rp, col, xdict_blocks(kern, m, s.h_tasks), long_t, xdict_cap_entries(dtype), true, P))
+    return HSPMV_OK;
+  if (mode < 0 && 2 * P.entries > P.in_kernel_nnz) return HSPMV_OK;  // too little reuse to pay
+  int rc;
+  if ((rc = dev_alloc(&s.d_c16, 2 * (size_t)std::max<int64_t>(nnz, 1), &s.bytes))) return rc;
+  if ((rc = dev_alloc(&s.d_xd_blk, 4 * P.blk.size(), &s.bytes))) return rc;
+  if ((rc = dev_alloc(&s.d_xd_runs, 4 * P.rec.size(), &s.bytes))) return rc;
+  if (nnz) HIP_TRY(hipMemcpy(s.d_c16, P.pos.data(), 2 * (size_t)nnz, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s.d_xd_blk, P.blk.data(), 4 * P.blk.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s.d_xd_runs, P.rec.data(), 4 * P.rec.size(), hipMemcpyHostToDevice));
+  s.A.col16 = s.d_c16;
+  s.A.cbase = nullptr;
+  s.A.cplanes = nullptr;
+  s.A.n_cplanes = 0;
+  s.xd_shape = kern;
+  s.xd_lds_bytes = (int32_t)((int64_t)P.tmax * (int64_t)sv);
+  s.xd_entries = P.entries;
+  s.xd_runs_n = (int64_t)P.rec.size() / 2;
+  return HSPMV_OK;
+}
+
 // Host-side tables that need the columns (built at upload, while they are
-// at hand): the CSR-3 packed tasks and the x windows of both row kernels.
-void build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, int64_t m) {
+// at hand): the CSR-3 packed tasks, the block x dictionaries, and (without
+// dictionaries) the 16-bit column offsets and the x windows of both row
+// kernels.
+int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int64_t n,
+                     int dtype, unsigned flags) {
   s.h_tasks.clear();
-  if (s.A.n_ssr > 0 && csr3_packed()) pack_csr3_tasks(s);
-  s.h_xwin = xwin_table(rp, col, m, nullptr);
+  if (s.A.n_ssr > 0 && csr3_packed()) pack_csr3_tasks(s.h_inner, s.A.m, s.h_tasks);
+  int rc;
+  if ((rc = build_xdict(s, rp, col, m, n, dtype, flags))) return rc;
+  s.h_xwin.clear();
   s.h_xwin_t.clear();
+  if (s.xd_shape) {  // col_span_bits: the planner's gather-regularity hint
+    s.A.col_span_bits = 1;
+    return HSPMV_OK;
+  }
+  bool c16 = false;
+  if ((rc = build_col16(s, col, rp[m], m, n, dtype, flags, &c16))) return rc;
+  s.h_xwin = xwin_table(rp, col, m, nullptr);
   if (!s.h_tasks.empty()) s.h_xwin_t = xwin_table(rp, col, m, &s.h_tasks);
+  return HSPMV_OK;
 }
 
 // Uploads rows [r0, r1) of A (and the matching slice of the maps) to shard s.
@@ -363,8 +566,6 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
   s.A.row_ptr = s.d_rp;
   s.A.col_idx = s.d_ci;
   s.A.val = s.d_val;
-  bool c16 = false;
-  if ((rc = build_col16(s, A->col_idx + k0, nnz, m, A->n, A->dtype, flags, &c16))) return rc;
   if (mp && mp->n_ssr > 0) {
     const int64_t nssr = ssr1 - ssr0;
     const int64_t sr0 = mp->outer[ssr0], sr1 = mp->outer[ssr1];
@@ -384,8 +585,7 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
     s.A.inner = s.d_inner;
     s.mean_rows_per_ssr = nssr ? (double)m / (double)nssr : 0.0;
   }
-  build_row_tables(s, rp.data(), A->col_idx + k0, m);
-  return HSPMV_OK;
+  return build_row_tables(s, rp.data(), A->col_idx + k0, m, A->n, A->dtype, flags);
 }
 
 // Host planner tables for one shard (needs s.h_rp, and s.h_outer/h_inner for
@@ -437,7 +637,23 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     s.A.cplanes = nullptr;
     s.A.n_cplanes = 0;
   }
-  if (s.A.col16) {
+  if (s.xd_shape) {
+    const bool fits = (s.xd_shape == kStream && s.plan.kernel == kStream && s.plan.groups == 1) ||
+                      (s.xd_shape == kCsr3 && s.plan.kernel == kCsr3 && !s.h_tasks.empty() &&
+                       s.plan.waves_per_block == 4);
+    if (fits) {
+      s.dp.xd_blk = s.d_xd_blk;
+      s.dp.xd_runs = s.d_xd_runs;
+      s.dp.xd_lds_bytes = s.xd_lds_bytes;
+      // index bytes: 2 instead of 4 per in-kernel nonzero, plus the tables;
+      // x: the staged entries instead of the distinct columns
+      const double sv = (double)dtype_size(dtype);
+      s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)(s.xd_runs_n * 2) -
+                    4.0 * (double)s.plan.blocks - sv * (double)(s.xd_entries - s.x_entries);
+    } else {  // planned for another block shape: the kernels read the 32-bit columns
+      s.A.col16 = nullptr;
+    }
+  } else if (s.A.col16) {
     const int64_t nb = (s.A.nnz + (int64_t(1) << kC16Shift) - 1) >> kC16Shift;
     s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)nb -
                   (double)s.A.n_cplanes * (double)(s.A.nnz - long_nnz) / 8.0;
@@ -593,8 +809,6 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
       for (int32_t c : cols)
         if (c < 0 || c >= A->n) return set_error(HSPMV_E_INVALID, "device col_idx %d out of [0, %lld)", c, (long long)A->n);
       s.x_entries = count_distinct_cols(cols.data(), A->nnz, A->n);
-      bool c16 = false;
-      if ((rc = build_col16(s, cols.data(), A->nnz, A->m, A->n, A->dtype, flags, &c16))) return rc;
     }
     if (maps && maps->n_ssr > 0) {
       std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
@@ -609,7 +823,7 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
       s.mean_rows_per_ssr = (double)A->m / (double)maps->n_ssr;
       h->n_ssr = maps->n_ssr; h->n_sr = maps->n_sr;
     }
-    build_row_tables(s, rp.data(), cols.data(), A->m);
+    if ((rc = build_row_tables(s, rp.data(), cols.data(), A->m, A->n, A->dtype, flags))) return rc;
     std::vector<int32_t>().swap(cols);
     const size_t sv = dtype_size(A->dtype);
     if ((rc = dev_alloc(&s.d_x, sv * (size_t)A->n, &s.bytes))) return rc;
@@ -912,6 +1126,39 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->col16 = s.A.col16 ? 1 + s.A.n_cplanes : 0;
   out->wave_tasks = s.plan.kernel == kCsr3 ? s.dp.n_tasks : 0;
   out->x_windows = s.dp.xwin ? 1 : 0;
+  out->x_dict = s.dp.xd_blk ? 1 : 0;
+  for (auto &sh : h->shards) out->x_dict_entries += sh.dp.xd_blk ? sh.xd_entries : 0;
+  return HSPMV_OK;
+}
+
+int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, unsigned flags,
+                     int64_t cap_entries, int64_t *n_blocks, int64_t *n_records, int32_t *blk,
+                     int32_t *runs, uint16_t *pos) {
+  clear_error();
+  if (!n_blocks || !n_records) return set_error(HSPMV_E_INVALID, "NULL output");
+  *n_blocks = 0;
+  *n_records = 0;
+  int rc;
+  if ((rc = validate_host_csr(A, true))) return rc;
+  if ((rc = validate_host_maps(maps, A->m))) return rc;
+  std::vector<int32_t> tasks;
+  const bool csr3 = maps && maps->n_ssr > 0;
+  if (csr3 && csr3_packed())
+    pack_csr3_tasks(std::vector<int32_t>(maps->inner, maps->inner + maps->n_sr + 1), (int32_t)A->m, tasks);
+  const int kern = kernel_for_tables(csr3 ? maps->n_ssr : 0, !tasks.empty(), flags);
+  if ((kern != kStream && kern != kCsr3) || A->m == 0) return HSPMV_OK;
+  if (cap_entries <= 0) cap_entries = xdict_cap_entries(A->dtype);
+  XdPlan P;
+  const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
+  const bool fill = blk || runs || pos;
+  if (!plan_xdict(A->row_ptr, A->col_idx, xdict_blocks(kern, A->m, tasks), long_t,
+                  std::min<int64_t>(cap_entries, 65536), fill, P))
+    return HSPMV_OK;  // some block exceeds the cap: no dictionary (n_blocks = 0)
+  *n_blocks = (int64_t)P.blk.size() - 1;
+  *n_records = (int64_t)P.blk.back();
+  if (blk) memcpy(blk, P.blk.data(), 4 * P.blk.size());
+  if (runs) memcpy(runs, P.rec.data(), 4 * P.rec.size());
+  if (pos && A->nnz) memcpy(pos, P.pos.data(), 2 * (size_t)A->nnz);
   return HSPMV_OK;
 }
 

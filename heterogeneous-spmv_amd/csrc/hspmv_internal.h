@@ -56,6 +56,14 @@ struct DevPlan {
   // {lo, w} (int32), w = 0 when the group's columns span more than kXWin
   // entries (then it gathers from global x)
   const void *xwin = nullptr;
+  // Block x dictionaries (STREAM with one group per wave: 256-row blocks;
+  // CSR3: blocks of four packed tasks): xd_blk[b], xd_blk[b+1] bound block
+  // b's {x_start, lds_off} run records in xd_runs (int2), the last a sentinel
+  // {0, entries}; col16 then holds each nonzero's position in the staged xs.
+  // xd_lds_bytes = the largest block's dictionary (dynamic LDS per block).
+  const int32_t *xd_blk = nullptr;
+  const void *xd_runs = nullptr;
+  int32_t xd_lds_bytes = 0;
 };
 
 struct LaunchPlan {

@@ -174,7 +174,7 @@ struct XWin {
 // C forms the products into LDS; then the row sums.  PF (software
 // pipelining): the next chunk's stage A is issued between this chunk's
 // stage B and C, so its latency overlaps the gather and the sums.
-template <typename T, bool NT, int U, bool PF, bool C16, bool XW>
+template <typename T, bool NT, int U, bool PF, bool C16, bool XW, bool XD>
 __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, int32_t end,
                                           int32_t long_t, const ColSrc &cs,
                                           const T *__restrict__ val,
@@ -192,7 +192,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
   const unsigned long long coopmask = __ballot(valid && !skip && len > kSerialMax);
   const bool serial = valid && !skip && len <= kSerialMax;
   const gchar *xb = uniform_ptr(x);
-  const bool inwin = XW && win.w > 0;
+  const bool inwin = (XW && win.w > 0) || XD;
   T acc = T(0);
   // Runs of consecutive non-split rows [a, b); normally one run = the group.
   int32_t a = g0;
@@ -207,7 +207,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
       const bool mine = serial && row >= a && row < b;
       int32_t col[U];
       T v[U];
-      const gchar *cb = C16 ? uniform_ptr(cs.c16 + kb) : uniform_ptr(cs.ci + kb);
+      const gchar *cb = (C16 || XD) ? uniform_ptr(cs.c16 + kb) : uniform_ptr(cs.ci + kb);
       const gchar *vb = uniform_ptr(val + kb);
       // (A raw-buffer form -- SGPR descriptors bounded to the run, no
       // clamp VALU -- measured 0-2.5 % slower in one-process A/B runs,
@@ -217,7 +217,9 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         for (int u = 0; u < U; ++u) {
           // clamp instead of branching: every load issues back to back
           const uint32_t j = (uint32_t)(c0 + min(u * kWave + lane, last));
-          if constexpr (C16) {
+          if constexpr (XD) {
+            col[u] = (int32_t)ld_off<NT, uint16_t>(cb, j * 2u);  // position in the block's xs
+          } else if constexpr (C16) {
             // col = base of the nonzero's 256-block + 16-bit offset.  The 64
             // lanes of a slice lie in at most two consecutive blocks: one
             // scalar load brings both bases (s_load, no vector memory op)
@@ -257,7 +259,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         if (inwin) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            xv[u] = win.xs[col[u] - win.lo];
+            xv[u] = XD ? win.xs[col[u]] : win.xs[col[u] - win.lo];
             vv[u] = v[u];
           }
         } else {
@@ -338,22 +340,77 @@ __device__ __forceinline__ void stage_xwin(T *xs, const T *__restrict__ x, int32
   wave_sync();
 }
 
+// Block x dictionary (XD): the x entries a workgroup's rows reference,
+// as runs of consecutive columns.  blk[b], blk[b+1] bound block b's records
+// in runs: {x_start, lds_off} per run, then a sentinel {0, total}; run i
+// stages x[x_start, x_start + len) at xs[lds_off ...], len = the next
+// record's lds_off - lds_off.  The col stream then holds each nonzero's
+// 16-bit position in xs (the host builds both, hspmv_api.cpp build_xdict).
+struct XDict {
+  const int32_t *blk;
+  const int2 *runs;
+};
+
+// The workgroup stages its dictionary into xs (NTH threads, contiguous loads
+// per run instead of one gather per nonzero) and waits at a block barrier.
+// Every wave of the block must call this (before any early return).
+template <typename T, int NTH>
+__device__ __forceinline__ void stage_xdict(T *xs, const T *__restrict__ x, const XDict &xd,
+                                            int64_t blk, int tid) {
+  constexpr int kBatch = 8;
+  const int64_t rr = sload_i64(xd.blk, (uint64_t)blk * 4u);
+  const int32_t r0 = (int32_t)rr;
+  const int32_t nr = (int32_t)(rr >> 32) - r0 - 1;  // runs (<= 63), then the sentinel
+  const int lane = tid & (kWave - 1);
+  int2 rec = make_int2(0, 0);
+  if (nr >= 0 && lane <= nr) rec = xd.runs[r0 + lane];
+  const int32_t total = nr >= 0 ? __builtin_amdgcn_readlane(rec.y, nr) : 0;
+  const int32_t delta = rec.x - rec.y;  // x index = xs index + delta inside the run
+  const gchar *xb = uniform_ptr(x);
+  for (int32_t e0 = 0; e0 < total; e0 += NTH * kBatch) {  // block-uniform
+    int32_t e[kBatch], d[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      e[j] = e0 + j * NTH + tid;
+      d[j] = 0;
+    }
+    for (int r = 0; r < nr; ++r) {  // runs are sorted by lds_off: the last run starting <= e
+      const int32_t o = __builtin_amdgcn_readlane(rec.y, r);
+      const int32_t dl = __builtin_amdgcn_readlane(delta, r);
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) d[j] = e[j] >= o ? dl : d[j];
+    }
+    T v[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j)
+      v[j] = ld_off<false, T>(xb, (uint32_t)(min(e[j], total - 1) + d[j]) * (uint32_t)sizeof(T));
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j)
+      if (e[j] < total) xs[e[j]] = v[j];
+  }
+  __syncthreads();
+}
+
 // STREAM: wave w walks `groups` consecutive 64-row groups starting at row
 // w * groups * 64, loading the next group's row pointers before streaming
 // the current one.  XW: groups whose x window (xwin[g] = {lo, w}) fits
 // kXWin entries gather from an LDS copy of it.
-template <typename T, bool NT, int U, bool PF, bool C16, bool XW>
+template <typename T, bool NT, int U, bool PF, bool C16, bool XW, bool XD>
 __global__ __launch_bounds__(256) void hspmv_csr_stream(
     int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups, int32_t y_nt,
-    const int32_t *__restrict__ rp, ColSrc cs, const int2 *__restrict__ xwin,
+    const int32_t *__restrict__ rp, ColSrc cs, const int2 *__restrict__ xwin, XDict xd,
     const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[4 * kWave * U];
   __shared__ T xlds[XW ? 4 * kXWin : 1];
+  extern __shared__ __attribute__((aligned(16))) unsigned char xdyn[];  // XD: the block's xs
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t blk = xcd_chunk_remap(blockIdx.x, gridDim.x, xcd_chunk);
+  // XD (groups == 1): the block's 256 rows share one staged dictionary; the
+  // only block barrier of the kernel is at the end of the staging.
+  if constexpr (XD) stage_xdict<T, 256>(reinterpret_cast<T *>(xdyn), x, xd, blk, threadIdx.x);
   int64_t g0 = (blk * 4 + wid) * (int64_t)groups * kWave;
-  if (g0 >= m) return;  // wave-uniform; no block barrier in this kernel
+  if (g0 >= m) return;  // wave-uniform
   const int64_t gend = min<int64_t>(g0 + (int64_t)groups * kWave, m);
   T *my = lds + wid * kWave * U;
   unsigned long long *ts = nullptr;
@@ -374,7 +431,7 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
 #endif
   while (true) {
     const int32_t g1 = (int32_t)min<int64_t>(g0 + kWave, gend);
-    XWin<T> win{nullptr, 0, 0};
+    XWin<T> win{XD ? reinterpret_cast<const T *>(xdyn) : nullptr, 0, 0};
     if constexpr (XW) {
       const int64_t wv = sload_i64(xwin, (uint64_t)(g0 / kWave) * 8u);
       win.lo = (int32_t)wv;
@@ -384,8 +441,8 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
     }
     int32_t nbeg = 0, nend = 0;
     if (g1 < gend) group_bounds(rp, g1, (int32_t)min<int64_t>(g1 + kWave, gend), lane, nbeg, nend);
-    wave_rows<T, NT, U, PF, C16, XW>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                     win, y_nt != 0, ts);
+    wave_rows<T, NT, U, PF, C16, XW, XD>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my,
+                                         lane, win, y_nt != 0, ts);
     ts = nullptr;  // trace the first group only
     if (g1 >= gend) break;
     g0 = g1;
@@ -394,17 +451,20 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
   }
 }
 
-template <typename T, bool NT, int U, bool PF, bool C16, int W, bool XW>
+template <typename T, bool NT, int U, bool PF, bool C16, int W, bool XW, bool XD>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, int32_t y_nt,
-    const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin,
+    const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin, XDict xd,
     const int32_t *__restrict__ rp, ColSrc cs, const T *__restrict__ val,
     const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[W * kWave * U];
   __shared__ T xlds[XW ? W * kXWin : 1];
+  extern __shared__ __attribute__((aligned(16))) unsigned char xdyn[];  // XD: the block's xs
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t blk = xcd_chunk_remap(blockIdx.x, gridDim.x, xcd_chunk);
+  // XD: the W packed tasks of the block share one staged dictionary
+  if constexpr (XD) stage_xdict<T, W * 64>(reinterpret_cast<T *>(xdyn), x, xd, blk, threadIdx.x);
   const int64_t t = blk * W + wid;
   if (t >= n_tasks) return;
 #if (HSPMV_DIAG & 8)
@@ -416,7 +476,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
   const int32_t r1 = (int32_t)(tb >> 32);
   if (r0 >= r1) return;
   T *my = lds + wid * kWave * U;
-  XWin<T> win{nullptr, 0, 0};
+  XWin<T> win{XD ? reinterpret_cast<const T *>(xdyn) : nullptr, 0, 0};
   if constexpr (XW) {  // the task's x window (packed tasks: <= 64 rows)
     const int64_t wv = sload_i64(xwin, (uint64_t)t * 8u);
     win.lo = (int32_t)wv;
@@ -439,8 +499,8 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     const int32_t g1 = min(g0 + kWave, r1);
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
-    wave_rows<T, NT, U, PF, C16, XW>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                     win, y_nt != 0, ts);
+    wave_rows<T, NT, U, PF, C16, XW, XD>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
+                                         win, y_nt != 0, ts);
     ts = nullptr;
     beg = nbeg;
     end = nend;
@@ -453,72 +513,94 @@ inline ColSrc col_src(const DevCSR &A) {
   return ColSrc{A.col_idx, A.col16, A.cbase, A.cplanes, A.n_cplanes, A.cplane_words};
 }
 
-template <typename T, bool NT, int U, bool PF, bool C16>
+template <typename T, bool NT, int U, bool PF, bool C16, bool XD>
 void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x, T *y,
                    hipStream_t st) {
   const T *val = static_cast<const T *>(A.val);
   const ColSrc cs = col_src(A);
-  const unsigned dyn = (unsigned)p.dyn_lds;  // occupancy experiments (HSPMV_DYNLDS)
+  const XDict xd{dp.xd_blk, reinterpret_cast<const int2 *>(dp.xd_runs)};
+  // dynamic LDS: the block's x dictionary (XD), or occupancy experiments (HSPMV_DYNLDS)
+  const unsigned dyn = XD ? (unsigned)dp.xd_lds_bytes : (unsigned)p.dyn_lds;
   if (p.kernel == kStream) {
     const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
-    if (xw)
-      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true>), dim3((unsigned)p.blocks),
-                         dim3(256), dyn, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk,
-                         (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs, xw, val, x, y);
+    if constexpr (XD)
+      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, false, false, true>),
+                         dim3((unsigned)p.blocks), dim3(256), dyn, st, A.m, dp.long_t,
+                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs,
+                         xw, xd, val, x, y);
+    else if (xw)
+      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true, false>),
+                         dim3((unsigned)p.blocks), dim3(256), dyn, st, A.m, dp.long_t,
+                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs,
+                         xw, xd, val, x, y);
     else
-      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false>), dim3((unsigned)p.blocks),
-                         dim3(256), dyn, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk,
-                         (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs, xw, val, x, y);
+      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false, false>),
+                         dim3((unsigned)p.blocks), dim3(256), dyn, st, A.m, dp.long_t,
+                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs,
+                         xw, xd, val, x, y);
     return;
   }
   const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
-#define HSPMV_CSR3(W, XW)                                                                     \
-  hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C16, W, XW>), dim3((unsigned)p.blocks),        \
+#define HSPMV_CSR3(W, C, XW, X)                                                               \
+  hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C, W, XW, X>), dim3((unsigned)p.blocks),      \
                      dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,     \
-                     (int32_t)p.y_nt, dp.task_start, xw, A.row_ptr, cs, val, x, y)
-  if (xw && p.waves_per_block == 4) {  // x windows: packed tasks only (4 per block)
-    HSPMV_CSR3(4, true);
+                     (int32_t)p.y_nt, dp.task_start, xw, xd, A.row_ptr, cs, val, x, y)
+  if constexpr (XD) {  // packed tasks only (4 per block)
+    HSPMV_CSR3(4, false, false, true);
     return;
-  }
-  switch (p.waves_per_block) {
-    case 1: HSPMV_CSR3(1, false); break;
-    case 2: HSPMV_CSR3(2, false); break;
-    case 4: HSPMV_CSR3(4, false); break;
-    default: HSPMV_CSR3(8, false); break;
+  } else {
+    if (xw && p.waves_per_block == 4) {  // x windows: packed tasks only (4 per block)
+      HSPMV_CSR3(4, C16, true, false);
+      return;
+    }
+    switch (p.waves_per_block) {
+      case 1: HSPMV_CSR3(1, C16, false, false); break;
+      case 2: HSPMV_CSR3(2, C16, false, false); break;
+      case 4: HSPMV_CSR3(4, C16, false, false); break;
+      default: HSPMV_CSR3(8, C16, false, false); break;
+    }
   }
 #undef HSPMV_CSR3
 }
 
-template <typename T, bool NT, bool PF, bool C16>
+template <typename T, bool NT, bool PF, bool C16, bool XD>
 hipError_t launch_rows_pf(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x,
                           T *y, hipStream_t st) {
   switch (p.u) {
-    case 2: launch_rows_u<T, NT, 2, PF, C16>(A, dp, p, x, y, st); break;
-    case 3: launch_rows_u<T, NT, 3, PF, C16>(A, dp, p, x, y, st); break;
-    case 4: launch_rows_u<T, NT, 4, PF, C16>(A, dp, p, x, y, st); break;
-    case 6: launch_rows_u<T, NT, 6, PF, C16>(A, dp, p, x, y, st); break;
-    case 8: launch_rows_u<T, NT, 8, PF, C16>(A, dp, p, x, y, st); break;
-    case 16: launch_rows_u<T, NT, 16, PF, C16>(A, dp, p, x, y, st); break;
+    case 2: launch_rows_u<T, NT, 2, PF, C16, XD>(A, dp, p, x, y, st); break;
+    case 3: launch_rows_u<T, NT, 3, PF, C16, XD>(A, dp, p, x, y, st); break;
+    case 4: launch_rows_u<T, NT, 4, PF, C16, XD>(A, dp, p, x, y, st); break;
+    case 6: launch_rows_u<T, NT, 6, PF, C16, XD>(A, dp, p, x, y, st); break;
+    case 8: launch_rows_u<T, NT, 8, PF, C16, XD>(A, dp, p, x, y, st); break;
+    case 16: launch_rows_u<T, NT, 16, PF, C16, XD>(A, dp, p, x, y, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-template <typename T, bool C16>
+template <typename T, bool C16, bool XD>
 hipError_t launch_rows_c(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x,
                          T *y, hipStream_t st) {
   if (p.nontemporal)
-    return p.prefetch ? launch_rows_pf<T, true, true, C16>(A, dp, p, x, y, st)
-                      : launch_rows_pf<T, true, false, C16>(A, dp, p, x, y, st);
-  return p.prefetch ? launch_rows_pf<T, false, true, C16>(A, dp, p, x, y, st)
-                    : launch_rows_pf<T, false, false, C16>(A, dp, p, x, y, st);
+    return p.prefetch ? launch_rows_pf<T, true, true, C16, XD>(A, dp, p, x, y, st)
+                      : launch_rows_pf<T, true, false, C16, XD>(A, dp, p, x, y, st);
+  return p.prefetch ? launch_rows_pf<T, false, true, C16, XD>(A, dp, p, x, y, st)
+                    : launch_rows_pf<T, false, false, C16, XD>(A, dp, p, x, y, st);
 }
 
+// XD (block x dictionaries) replaces both the 32-bit columns and the col16
+// offsets: its col stream is the 16-bit xs positions.
 template <typename T>
 hipError_t launch_rows(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x, T *y,
                        hipStream_t st) {
-  return A.col16 ? launch_rows_c<T, true>(A, dp, p, x, y, st)
-                 : launch_rows_c<T, false>(A, dp, p, x, y, st);
+  if (dp.xd_blk) {
+    if (!A.col16 || (p.kernel == kStream && p.groups != 1) ||
+        (p.kernel == kCsr3 && (!dp.task_start || p.waves_per_block != 4)))
+      return hipErrorInvalidValue;  // the host built the dictionary for another block shape
+    return launch_rows_c<T, false, true>(A, dp, p, x, y, st);
+  }
+  return A.col16 ? launch_rows_c<T, true, false>(A, dp, p, x, y, st)
+                 : launch_rows_c<T, false, false>(A, dp, p, x, y, st);
 }
 
 }  // namespace dev

@@ -110,7 +110,8 @@ class Info(C.Structure):
                 ("flops", C.c_double), ("device_bytes", C.c_int64), ("chunk_u", C.c_int32),
                 ("n_split_rows", C.c_int32), ("xcd_remap", C.c_int32), ("groups_per_wave", C.c_int32),
                 ("x_entries", C.c_int64), ("format_bytes", C.c_double), ("col16", C.c_int32),
-                ("wave_tasks", C.c_int32), ("x_windows", C.c_int32), ("pad_", C.c_int32)]
+                ("wave_tasks", C.c_int32), ("x_windows", C.c_int32), ("x_dict", C.c_int32),
+                ("x_dict_entries", C.c_int64)]
 
 
 _P = C.c_void_p
@@ -145,6 +146,8 @@ SIGNATURES = {
                                          C.POINTER(Csr3Buf), _P]),
     "hspmv_csr3_params": (C.c_int, [C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hspmv_partition_rows": (C.c_int, [C.c_int64, _P, C.POINTER(Csr3Maps), C.c_int, _P]),
+    "hspmv_xdict_plan": (C.c_int, [C.POINTER(Csr), C.POINTER(Csr3Maps), C.c_uint, C.c_int64,
+                                   C.POINTER(C.c_int64), C.POINTER(C.c_int64), _P, _P, _P]),
     "hspmv_alg_bytes": (C.c_double, [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int64]),
     "hspmv_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "hspmv_last_error": (C.c_char_p, []),

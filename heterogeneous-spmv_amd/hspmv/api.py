@@ -229,6 +229,29 @@ def partition_rows(row_ptr: np.ndarray, parts: int, maps: Optional[Csr3Maps] = N
     return out
 
 
+def xdict_plan(A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, kernel: str = "auto",
+               cap_entries: int = 0, split: bool = True):
+    """Block x dictionaries the library would build for A (hspmv_xdict_plan):
+    (blk, runs, pos) with runs as an (n_records, 2) array of {x_start,
+    lds_off}, or None when some workgroup exceeds cap_entries (0 = the
+    library's LDS cap for A's dtype)."""
+    cs = A.c_struct()
+    ms = maps.c_struct() if maps is not None else None
+    flags = _KERNELS[kernel] | (0 if split else _lib.FLAG_NO_SPLIT)
+    nb, nr = C.c_int64(), C.c_int64()
+    L = lib()
+    args = (C.byref(cs), C.byref(ms) if ms is not None else None, flags, int(cap_entries))
+    check(L.hspmv_xdict_plan(*args, C.byref(nb), C.byref(nr), None, None, None), "xdict_plan")
+    if nb.value == 0:
+        return None
+    blk = np.empty(nb.value + 1, np.int32)
+    runs = np.empty((nr.value, 2), np.int32)
+    pos = np.zeros(max(A.nnz, 1), np.uint16)
+    check(L.hspmv_xdict_plan(*args, C.byref(nb), C.byref(nr), _ptr(blk), _ptr(runs), _ptr(pos)),
+          "xdict_plan")
+    return blk, runs, pos[:A.nnz]
+
+
 def alg_bytes(m: int, n: int, nnz: int, dtype, n_ssr: int = 0, n_sr: int = 0) -> float:
     return float(lib().hspmv_alg_bytes(m, n, nnz, dtype_code(dtype), n_ssr, n_sr))
 

@@ -126,7 +126,10 @@ typedef struct {
   int32_t x_windows;  /* STREAM/CSR3: 1 = row groups whose columns span
                          <= 256 entries gather from an LDS copy of that x
                          window; 0 = every gather from global x (GPU 0)     */
-  int32_t pad_;
+  int32_t x_dict;     /* 1 = block x dictionaries: each workgroup stages the
+                         x runs its rows reference in LDS and the column
+                         stream holds 16-bit positions in it (GPU 0)        */
+  int64_t x_dict_entries; /* x entries staged per SpMV (all GPUs; 0 = none) */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
@@ -285,6 +288,22 @@ int hspmv_partition_rows(int64_t m, const int32_t *row_ptr,
  * where n = the x entries the SpMV reads, i.e. the number of distinct
  * columns (the matrix width when every column holds a nonzero; much less for
  * a row-range shard of a banded matrix -- hspmv_info.x_entries). */
+/* Block x dictionaries (host planner; hspmv_create builds the same tables
+ * when it uses them, see hspmv_info.x_dict).  The row kernel's workgroups
+ * (STREAM: 256 consecutive rows; CSR3 with maps: four consecutive packed
+ * wave tasks) each stage the x entries their rows reference -- runs of
+ * consecutive columns, gaps of <= 8 bridged, <= 63 runs -- in LDS, and every
+ * nonzero's column becomes a 16-bit position in that copy.  Outputs:
+ * blk[n_blocks+1] record ranges; runs[2*n_records] = {x_start, lds_off} per
+ * run, then a sentinel {0, entries} per block; pos[nnz] (0 for split rows,
+ * > 4096 nonzeros, unless HSPMV_FLAG_NO_SPLIT).  So x[col[k]] ==
+ * staged_b[pos[k]] with staged_b[lds_off + i] = x[x_start + i].  Call with
+ * NULL buffers for the sizes.  *n_blocks = 0: some block needs more than
+ * cap_entries (<= 0: the library's LDS cap for A's dtype), so no dictionary.
+ * Not a reference interface: the test and diagnostic view of the format. */
+int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, unsigned flags,
+                     int64_t cap_entries, int64_t *n_blocks, int64_t *n_records,
+                     int32_t *blk, int32_t *runs, uint16_t *pos);
 double hspmv_alg_bytes(int64_t m, int64_t n, int64_t nnz, int dtype,
                        int64_t n_ssr, int64_t n_sr);
 int hspmv_device_count(int *count);

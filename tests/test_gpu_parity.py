@@ -410,3 +410,59 @@ def test_col16_offsets_bitwise_and_fallback():
     A = gen.laplace2d(100, 100)
     _, iv = gpu_spmv(A, gen.rand_x(A.n, 1), kernel="vector", col16=True)
     assert iv["col16"] == 0
+
+
+def _few_random(m, n, per_row, seed, dtype=np.float64):
+    """per_row random (sorted) columns per row: hundreds of column runs per
+    256-row block, so the dictionary builder must bridge gaps."""
+    rng = np.random.default_rng(seed)
+    cols = np.sort(rng.choice(n, size=(m, per_row), replace=True), axis=1)
+    rp = np.arange(0, m * per_row + 1, per_row, dtype=np.int32)
+    return hspmv.CsrMatrix(m, n, rp, cols.reshape(-1).astype(np.int32),
+                           rng.uniform(-1, 1, m * per_row).astype(dtype))
+
+
+def test_xdict_bitwise_and_fallback(monkeypatch):
+    """Block x dictionaries (HSPMV_XDICT=1 forces them on these small
+    matrices): each workgroup stages the x runs its rows reference in LDS
+    and gathers from there through 16-bit positions.  y is bit-identical to
+    the 32-bit-column path through STREAM, CSR3 (packed tasks), prefetch,
+    nontemporal loads, U = 2 and split rows, in fp64 and fp32; a matrix whose
+    blocks exceed the LDS cap falls back (x_dict = 0) with the same y."""
+    big = str(64 * 1024)  # LDS bytes per block (default cap: 20 KiB)
+    cases = [(gen.laplace2d(300, 200), True, None),
+             (gen.stencil27(20), True, None),
+             (gen.banded(30000, per_row=10, half=32, seed=5), True, None),
+             (_split_row_matrix(), None, big),
+             (gen.laplace2d(1, 1), True, None),
+             (gen.powerlaw(200000, seed=3, dtype=np.float64), False, None),   # > cap: off
+             (_few_random(3000, 8000, 2, 4), None, big)]                    # gap bridging
+    for A, want, cap in cases:
+        if cap:
+            monkeypatch.setenv("HSPMV_XDICT_CAP", cap)
+        else:
+            monkeypatch.delenv("HSPMV_XDICT_CAP", raising=False)
+        for dt in (np.float64, np.float32):
+            Ad = A.astype(dt)
+            x = gen.rand_x(A.n, 9).astype(dt)
+            maps = hspmv.build_csr3_maps(Ad, 20, 10)
+            for kw, mp in [(dict(kernel="stream"), None), (dict(kernel="stream", prefetch=True), None),
+                           (dict(kernel="csr3"), maps), (dict(kernel="stream", chunk_u=2), None),
+                           (dict(kernel="csr3", nontemporal=True), maps)]:
+                monkeypatch.setenv("HSPMV_XDICT", "1")
+                yd, idd = gpu_spmv(Ad, x, mp, **kw)
+                monkeypatch.setenv("HSPMV_XDICT", "0")
+                y0, i0 = gpu_spmv(Ad, x, mp, col16=False, **kw)
+                assert i0["x_dict"] == 0 and i0["x_dict_entries"] == 0
+                if want is not None and not (want is False and dt == np.float32):
+                    assert idd["x_dict"] == int(want), (kw, dt, idd["x_dict"])
+                if idd["x_dict"]:
+                    assert idd["x_dict_entries"] > 0 and idd["col16"] == 1
+                assert np.array_equal(yd.view(np.uint8), y0.view(np.uint8)), (kw, dt)
+            if dt == np.float64:
+                check_fp64(Ad, x, yd, exact_rows=short_rows(Ad))
+    monkeypatch.delenv("HSPMV_XDICT")
+    # default on these small (Infinity-Cache-resident) matrices: no dictionary
+    A = gen.stencil27(20)
+    _, idef = gpu_spmv(A, gen.rand_x(A.n, 1))
+    assert idef["x_dict"] == 0
