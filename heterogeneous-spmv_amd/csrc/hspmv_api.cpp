@@ -474,12 +474,17 @@ int64_t xdict_cap_entries(int dtype) {
                            65536);
 }
 
+// Auto mode also leaves banded matrices to the x windows (have_xwin: the
+// row kernel's window table qualified): on C4's shard the per-wave windows
+// need no block barrier and were 7 % faster than the dictionaries
+// (53.8 vs 57.9 us, profiles/r01_ab_xdict.jsonl).
 int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int64_t n, int dtype,
-                unsigned flags) {
+                unsigned flags, bool have_xwin) {
   s.xd_shape = 0;
   const char *env = getenv("HSPMV_XDICT");
   const int mode = env ? atoi(env) : -1;  // -1 auto, 0 off, 1 on when it fits
   if (mode == 0 || (flags & HSPMV_FLAG_NO_COL16) || m == 0) return HSPMV_OK;
+  if (mode < 0 && have_xwin) return HSPMV_OK;
   const int kern = kernel_for_tables(s.A.n_ssr, !s.h_tasks.empty(), flags);
   if (kern != kStream && kern != kCsr3) return HSPMV_OK;
   if (kern == kStream && ((flags >> 29) & 0x7u) > 1) return HSPMV_OK;  // groups != 1
@@ -518,18 +523,21 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, int64_t m,
                      int dtype, unsigned flags) {
   s.h_tasks.clear();
   if (s.A.n_ssr > 0 && csr3_packed()) pack_csr3_tasks(s.h_inner, s.A.m, s.h_tasks);
-  int rc;
-  if ((rc = build_xdict(s, rp, col, m, n, dtype, flags))) return rc;
-  s.h_xwin.clear();
+  s.h_xwin = xwin_table(rp, col, m, nullptr);
   s.h_xwin_t.clear();
+  if (!s.h_tasks.empty()) s.h_xwin_t = xwin_table(rp, col, m, &s.h_tasks);
+  const int kern = kernel_for_tables(s.A.n_ssr, !s.h_tasks.empty(), flags);
+  const bool have_xwin = kern == kCsr3 ? !s.h_xwin_t.empty() : !s.h_xwin.empty();
+  int rc;
+  if ((rc = build_xdict(s, rp, col, m, n, dtype, flags, have_xwin))) return rc;
   if (s.xd_shape) {  // col_span_bits: the planner's gather-regularity hint
+    s.h_xwin.clear();
+    s.h_xwin_t.clear();
     s.A.col_span_bits = 1;
     return HSPMV_OK;
   }
   bool c16 = false;
   if ((rc = build_col16(s, col, rp[m], m, n, dtype, flags, &c16))) return rc;
-  s.h_xwin = xwin_table(rp, col, m, nullptr);
-  if (!s.h_tasks.empty()) s.h_xwin_t = xwin_table(rp, col, m, &s.h_tasks);
   return HSPMV_OK;
 }
 

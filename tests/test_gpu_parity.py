@@ -253,7 +253,9 @@ def test_config_c4_banded_shard_fp64():
     x = gen.rand_x(m, 11)
     y, info = gpu_spmv(A, x)
     check_fp64(A, x, y, exact_rows=slice(None))
-    assert info["x_windows"] == 1  # one window of <= 128 columns per group
+    # the gathers are staged in LDS: one x window of <= 256 columns per
+    # group, or (the default for HBM-resident matrices) a block x dictionary
+    assert info["x_windows"] == 1 or info["x_dict"] == 1
 
 
 def test_config_c5_powerlaw_csr3_fp32():
