@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <atomic>
 #include <chrono>
@@ -61,6 +62,10 @@ struct Shard {
   int xd_shape = 0;                  // 0 none, kStream (256-row blocks), kCsr3 (4 packed tasks)
   int64_t xd_entries = 0;            // x entries staged per SpMV (all blocks)
   int64_t xd_runs_n = 0;             // run records incl. sentinels
+  int32_t *d_slab_rp = nullptr;      // x slabs (build_xslabs): per-slab row pointers,
+  int32_t *d_slab_col = nullptr;     // slab-major columns and values
+  void *d_slab_val = nullptr;
+  int32_t n_slabs = 0;
   std::vector<int32_t> h_xwin;       // built at upload (host columns at hand)
   std::vector<int32_t> h_xwin_t;     // the same per packed CSR-3 task
   void *d_val = nullptr;
@@ -132,6 +137,9 @@ void free_shard(Shard &s, bool borrowed) {
   (void)hipFree(s.d_xwin);
   (void)hipFree(s.d_xd_blk);
   (void)hipFree(s.d_xd_runs);
+  (void)hipFree(s.d_slab_rp);
+  (void)hipFree(s.d_slab_col);
+  (void)hipFree(s.d_slab_val);
   (void)hipFree(s.d_task);
   (void)hipFree(s.d_long_row);
   (void)hipFree(s.d_long_cstart);
@@ -515,20 +523,141 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
   return HSPMV_OK;
 }
 
+// x slabs.  When the gathers are irregular (a 64-row group's columns span
+// more than an XCD's 4 MiB L2 of x) and x itself exceeds the L2, nearly
+// every gather misses L2 and pulls a whole line from the Infinity Fabric
+// for 4-8 useful bytes (C5, power-law with random columns: ~48 M such
+// misses, 443 us for 400 MB of matrix).  Cutting the columns into slabs
+// of <= kSlabBytes of x and running the row kernel once per slab over a
+// slab-major copy keeps each pass's gathers inside one L2-resident slice;
+// the price per extra pass is one more row-pointer array and a y read +
+// write.  Pass b > 0 starts each row from the y of pass b-1, so a row's
+// products are still added left to right from 0 (bit-identical to
+// omp_spmv for rows of <= 32 nonzeros per slab segment) -- which needs the
+// row's columns to be non-decreasing slab by slab (sorted rows; checked).
+// HSPMV_XSLABS=0 disables, =B forces B slabs; HSPMV_XSLAB_BYTES moves the
+// slab size.
+constexpr double kSlabBytes = 2.0 * 1024 * 1024;
+constexpr int kMaxSlabs = 32;
+
+int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
+                 int64_t n, int dtype, unsigned flags) {
+  s.n_slabs = 0;
+  const char *env = getenv("HSPMV_XSLABS");
+  const int forced = env ? atoi(env) : -1;  // -1 auto, 0 off, B slabs
+  if (forced == 0 || !val || m == 0 || n == 0 || (flags & 0xFu) == kVector) return HSPMV_OK;
+  const int64_t nnz = rp[m];
+  const double sv = (double)dtype_size(dtype);
+  double slab_bytes = kSlabBytes;
+  if (const char *e = getenv("HSPMV_XSLAB_BYTES")) slab_bytes = std::max(4096.0, atof(e));
+  int B = forced > 0 ? forced : (int)std::ceil((double)n * sv / slab_bytes);
+  B = (int)std::min<int64_t>(std::min(B, kMaxSlabs), n);
+  if (B < 2) return HSPMV_OK;
+  const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
+  const int64_t W = (n + B - 1) / B;  // columns per slab
+  const int64_t ng = (m + 63) / 64;
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, m / 65536));
+  auto par = [&](auto &&body) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back([&, t]() { body(t); });
+    for (auto &x : th) x.join();
+  };
+  if (forced < 0) {
+    const double footprint = (double)nnz * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv;
+    if (footprint <= kMallResident || (double)n * sv <= 4.0 * 1024 * 1024) return HSPMV_OK;
+    // irregular: the median 64-row group gathers over more than an L2 of x
+    std::vector<int64_t> wide((size_t)nt, 0), nonempty((size_t)nt, 0);
+    par([&](int t) {
+      for (int64_t g = ng * t / nt; g < ng * (t + 1) / nt; ++g) {
+        const int64_t k0 = rp[64 * g], k1 = rp[std::min(m, 64 * g + 64)];
+        if (k1 <= k0) continue;
+        int32_t lo = col[k0], hi = col[k0];
+        for (int64_t k = k0 + 1; k < k1; ++k) {
+          lo = std::min(lo, col[k]);
+          hi = std::max(hi, col[k]);
+        }
+        ++nonempty[(size_t)t];
+        if ((double)(hi - lo + 1) * sv > 4.0 * 1024 * 1024) ++wide[(size_t)t];
+      }
+    });
+    int64_t nw = 0, ne = 0;
+    for (int t = 0; t < nt; ++t) { nw += wide[(size_t)t]; ne += nonempty[(size_t)t]; }
+    if (2 * nw <= ne) return HSPMV_OK;
+  }
+  // per (slab, row) segment lengths; rows must be slab-monotone
+  std::vector<int32_t> srp((size_t)B * (size_t)(m + 1), 0);
+  std::atomic<bool> unsorted{false};
+  par([&](int t) {
+    for (int64_t r = m * t / nt; r < m * (t + 1) / nt; ++r) {
+      const int32_t k0 = rp[r], k1 = rp[r + 1];
+      if (k1 - k0 > long_t) continue;  // split rows: empty segments
+      int64_t prev = 0;
+      for (int32_t k = k0; k < k1; ++k) {
+        const int64_t b = col[k] / W;
+        if (b < prev) { unsorted = true; return; }
+        prev = b;
+        ++srp[(size_t)b * (size_t)(m + 1) + (size_t)r + 1];
+      }
+    }
+  });
+  if (unsorted) return HSPMV_OK;
+  int64_t base = 0;  // slab-major offsets
+  for (int b = 0; b < B; ++b) {
+    int32_t *p = srp.data() + (size_t)b * (size_t)(m + 1);
+    p[0] = (int32_t)base;
+    for (int64_t r = 0; r < m; ++r) p[r + 1] += p[r];
+    base = p[m];
+  }
+  const int64_t snnz = base;  // in-kernel nonzeros (split rows excluded)
+  std::vector<int32_t> scol((size_t)std::max<int64_t>(snnz, 1));
+  std::vector<char> sval((size_t)std::max<int64_t>(snnz, 1) * (size_t)sv);
+  par([&](int t) {
+    for (int64_t r = m * t / nt; r < m * (t + 1) / nt; ++r) {
+      const int32_t k0 = rp[r], k1 = rp[r + 1];
+      if (k1 - k0 > long_t) continue;
+      int32_t k = k0;
+      for (int b = 0; b < B; ++b) {
+        const int32_t *p = srp.data() + (size_t)b * (size_t)(m + 1);
+        for (int32_t o = p[r]; o < p[r + 1]; ++o, ++k) {
+          scol[(size_t)o] = col[k];
+          memcpy(sval.data() + (size_t)o * (size_t)sv, (const char *)val + (size_t)k * (size_t)sv,
+                 (size_t)sv);
+        }
+      }
+    }
+  });
+  int rc;
+  if ((rc = dev_alloc(&s.d_slab_rp, 4 * srp.size(), &s.bytes))) return rc;
+  if ((rc = dev_alloc(&s.d_slab_col, 4 * scol.size(), &s.bytes))) return rc;
+  if ((rc = dev_alloc(&s.d_slab_val, sval.size(), &s.bytes))) return rc;
+  HIP_TRY(hipMemcpy(s.d_slab_rp, srp.data(), 4 * srp.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s.d_slab_col, scol.data(), 4 * scol.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s.d_slab_val, sval.data(), sval.size(), hipMemcpyHostToDevice));
+  s.n_slabs = B;
+  return HSPMV_OK;
+}
+
 // Host-side tables that need the columns (built at upload, while they are
 // at hand): the CSR-3 packed tasks, the block x dictionaries, and (without
 // dictionaries) the 16-bit column offsets and the x windows of both row
 // kernels.
-int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int64_t n,
-                     int dtype, unsigned flags) {
+int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
+                     int64_t n, int dtype, unsigned flags) {
   s.h_tasks.clear();
   if (s.A.n_ssr > 0 && csr3_packed()) pack_csr3_tasks(s.h_inner, s.A.m, s.h_tasks);
+  s.h_xwin.clear();
+  s.h_xwin_t.clear();
+  int rc;
+  if ((rc = build_xslabs(s, rp, col, val, m, n, dtype, flags))) return rc;
+  if (s.n_slabs) {  // slab passes read 32-bit columns from global x
+    s.A.col_span_bits = 31;
+    return HSPMV_OK;
+  }
   s.h_xwin = xwin_table(rp, col, m, nullptr);
   s.h_xwin_t.clear();
   if (!s.h_tasks.empty()) s.h_xwin_t = xwin_table(rp, col, m, &s.h_tasks);
   const int kern = kernel_for_tables(s.A.n_ssr, !s.h_tasks.empty(), flags);
   const bool have_xwin = kern == kCsr3 ? !s.h_xwin_t.empty() : !s.h_xwin.empty();
-  int rc;
   if ((rc = build_xdict(s, rp, col, m, n, dtype, flags, have_xwin))) return rc;
   if (s.xd_shape) {  // col_span_bits: the planner's gather-regularity hint
     s.h_xwin.clear();
@@ -593,7 +722,8 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
     s.A.inner = s.d_inner;
     s.mean_rows_per_ssr = nssr ? (double)m / (double)nssr : 0.0;
   }
-  return build_row_tables(s, rp.data(), A->col_idx + k0, m, A->n, A->dtype, flags);
+  return build_row_tables(s, rp.data(), A->col_idx + k0, (const char *)A->val + sv * k0, m, A->n,
+                          A->dtype, flags);
 }
 
 // Host planner tables for one shard (needs s.h_rp, and s.h_outer/h_inner for
@@ -665,6 +795,15 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     const int64_t nb = (s.A.nnz + (int64_t(1) << kC16Shift) - 1) >> kC16Shift;
     s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)nb -
                   (double)s.A.n_cplanes * (double)(s.A.nnz - long_nnz) / 8.0;
+  }
+  if (s.n_slabs && (s.plan.kernel == kStream || s.plan.kernel == kCsr3)) {
+    s.dp.n_slabs = s.n_slabs;
+    s.dp.slab_rp = s.d_slab_rp;
+    s.dp.slab_col = s.d_slab_col;
+    s.dp.slab_val = s.d_slab_val;
+    // per extra pass: one more row-pointer array, and y read back + rewritten
+    const double sv = (double)dtype_size(dtype);
+    s.c16_saved = -(double)(s.n_slabs - 1) * (4.0 * (double)(m + 1) + 2.0 * sv * (double)m);
   }
   const std::vector<int32_t> &xw = s.plan.kernel == kStream ? s.h_xwin : s.h_xwin_t;
   if ((s.plan.kernel == kStream || (s.plan.kernel == kCsr3 && !s.h_tasks.empty())) && !xw.empty()) {
@@ -831,7 +970,9 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
       s.mean_rows_per_ssr = (double)A->m / (double)maps->n_ssr;
       h->n_ssr = maps->n_ssr; h->n_sr = maps->n_sr;
     }
-    if ((rc = build_row_tables(s, rp.data(), cols.data(), A->m, A->n, A->dtype, flags))) return rc;
+    // (device values are not copied back: no x slabs for borrowed matrices)
+    if ((rc = build_row_tables(s, rp.data(), cols.data(), nullptr, A->m, A->n, A->dtype, flags)))
+      return rc;
     std::vector<int32_t>().swap(cols);
     const size_t sv = dtype_size(A->dtype);
     if ((rc = dev_alloc(&s.d_x, sv * (size_t)A->n, &s.bytes))) return rc;
@@ -1135,6 +1276,7 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->wave_tasks = s.plan.kernel == kCsr3 ? s.dp.n_tasks : 0;
   out->x_windows = s.dp.xwin ? 1 : 0;
   out->x_dict = s.dp.xd_blk ? 1 : 0;
+  out->x_slabs = s.dp.n_slabs;
   for (auto &sh : h->shards) out->x_dict_entries += sh.dp.xd_blk ? sh.xd_entries : 0;
   return HSPMV_OK;
 }

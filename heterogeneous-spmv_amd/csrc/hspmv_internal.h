@@ -64,6 +64,16 @@ struct DevPlan {
   const int32_t *xd_blk = nullptr;
   const void *xd_runs = nullptr;
   int32_t xd_lds_bytes = 0;
+  // x slabs (irregular gathers, x larger than an XCD's L2): the columns are
+  // cut into n_slabs equal ranges and the row kernel runs
+  // once per slab over a slab-major copy of the matrix -- pass b reads rows
+  // [slab_rp[b*(m+1) + r], slab_rp[b*(m+1) + r + 1]) of slab_col/slab_val,
+  // so its gathers stay inside one L2-sized slice of x.  Split rows have
+  // empty slab segments (the split-row kernels sum them from the CSR).
+  int32_t n_slabs = 0;
+  const int32_t *slab_rp = nullptr;
+  const int32_t *slab_col = nullptr;
+  const void *slab_val = nullptr;
 };
 
 struct LaunchPlan {
@@ -77,6 +87,7 @@ struct LaunchPlan {
   int32_t dyn_lds = 0;     // extra dynamic LDS per block (occupancy experiments)
   int32_t xcd_chunk = 1;   // blocks per XCD turn (1 = dispatch order; see xcd_chunk_remap)
   int32_t groups = 1;      // STREAM: 64-row groups per wave (next group's rp prefetched)
+  int32_t carry = 0;       // STREAM/CSR3: rows start from y (x-slab passes after the first)
   int64_t blocks = 0;
 };
 

@@ -180,7 +180,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
                                           const T *__restrict__ val,
                                           const T *__restrict__ x,
                                           T *__restrict__ y, T *lds, int lane,
-                                          const XWin<T> &win, bool y_nt,
+                                          const XWin<T> &win, bool y_nt, bool carry,
                                           unsigned long long *ts = nullptr) {
   const int32_t row = g0 + lane;
   const bool valid = row < g1;
@@ -193,7 +193,9 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
   const bool serial = valid && !skip && len <= kSerialMax;
   const gchar *xb = uniform_ptr(x);
   const bool inwin = (XW && win.w > 0) || XD;
-  T acc = T(0);
+  // x slabs: passes after the first continue each row's sum from y, so a
+  // row's products are still added left to right from 0 across the passes
+  T acc = (carry && valid && !skip) ? y[row] : T(0);
   // Runs of consecutive non-split rows [a, b); normally one run = the group.
   int32_t a = g0;
   while (a < g1) {
@@ -397,7 +399,7 @@ __device__ __forceinline__ void stage_xdict(T *xs, const T *__restrict__ x, cons
 // kXWin entries gather from an LDS copy of it.
 template <typename T, bool NT, int U, bool PF, bool C16, bool XW, bool XD>
 __global__ __launch_bounds__(256) void hspmv_csr_stream(
-    int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups, int32_t y_nt,
+    int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups, int32_t y_nt, int32_t carry,
     const int32_t *__restrict__ rp, ColSrc cs, const int2 *__restrict__ xwin, XDict xd,
     const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[4 * kWave * U];
@@ -442,7 +444,7 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
     int32_t nbeg = 0, nend = 0;
     if (g1 < gend) group_bounds(rp, g1, (int32_t)min<int64_t>(g1 + kWave, gend), lane, nbeg, nend);
     wave_rows<T, NT, U, PF, C16, XW, XD>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my,
-                                         lane, win, y_nt != 0, ts);
+                                         lane, win, y_nt != 0, carry != 0, ts);
     ts = nullptr;  // trace the first group only
     if (g1 >= gend) break;
     g0 = g1;
@@ -453,7 +455,7 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
 
 template <typename T, bool NT, int U, bool PF, bool C16, int W, bool XW, bool XD>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
-    int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, int32_t y_nt,
+    int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, int32_t y_nt, int32_t carry,
     const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin, XDict xd,
     const int32_t *__restrict__ rp, ColSrc cs, const T *__restrict__ val,
     const T *__restrict__ x, T *__restrict__ y) {
@@ -500,7 +502,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
     wave_rows<T, NT, U, PF, C16, XW, XD>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                         win, y_nt != 0, ts);
+                                         win, y_nt != 0, carry != 0, ts);
     ts = nullptr;
     beg = nbeg;
     end = nend;
@@ -526,17 +528,17 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
     if constexpr (XD)
       hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, false, false, true>),
                          dim3((unsigned)p.blocks), dim3(256), dyn, st, A.m, dp.long_t,
-                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs,
+                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
                          xw, xd, val, x, y);
     else if (xw)
       hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true, false>),
                          dim3((unsigned)p.blocks), dim3(256), dyn, st, A.m, dp.long_t,
-                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs,
+                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
                          xw, xd, val, x, y);
     else
       hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false, false>),
                          dim3((unsigned)p.blocks), dim3(256), dyn, st, A.m, dp.long_t,
-                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, A.row_ptr, cs,
+                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
                          xw, xd, val, x, y);
     return;
   }
@@ -544,7 +546,7 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
 #define HSPMV_CSR3(W, C, XW, X)                                                               \
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C, W, XW, X>), dim3((unsigned)p.blocks),      \
                      dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,     \
-                     (int32_t)p.y_nt, dp.task_start, xw, xd, A.row_ptr, cs, val, x, y)
+                     (int32_t)p.y_nt, p.carry, dp.task_start, xw, xd, A.row_ptr, cs, val, x, y)
   if constexpr (XD) {  // packed tasks only (4 per block)
     HSPMV_CSR3(4, false, false, true);
     return;

@@ -156,10 +156,28 @@ hipError_t launch_typed(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p,
       return hipGetLastError();  // the vector kernel sums split rows itself
     case kStream:
     case kCsr3:
-      if constexpr (sizeof(T) == 8)
+      if (dp.n_slabs > 0) {  // one pass per x slab, each continuing the rows from y
+        DevCSR As = A;
+        As.col_idx = dp.slab_col;
+        As.val = dp.slab_val;
+        As.col16 = nullptr;
+        As.cbase = nullptr;
+        As.cplanes = nullptr;
+        As.n_cplanes = 0;
+        LaunchPlan ps = p;
+        for (int32_t b = 0; b < dp.n_slabs && e == hipSuccess; ++b) {
+          As.row_ptr = dp.slab_rp + (size_t)b * (size_t)(A.m + 1);
+          ps.carry = b > 0;
+          if constexpr (sizeof(T) == 8)
+            e = launch_rows_f64(As, dp, ps, x, y, st);
+          else
+            e = launch_rows_f32(As, dp, ps, x, y, st);
+        }
+      } else if constexpr (sizeof(T) == 8) {
         e = launch_rows_f64(A, dp, p, x, y, st);
-      else
+      } else {
         e = launch_rows_f32(A, dp, p, x, y, st);
+      }
       if (e != hipSuccess) return e;
       break;
     default:

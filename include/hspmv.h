@@ -130,6 +130,9 @@ typedef struct {
                          x runs its rows reference in LDS and the column
                          stream holds 16-bit positions in it (GPU 0)        */
   int64_t x_dict_entries; /* x entries staged per SpMV (all GPUs; 0 = none) */
+  int32_t x_slabs;    /* STREAM/CSR3: 0, or the number of column slabs the
+                         row kernel runs over, one pass each, so irregular
+                         gathers stay in an L2-sized slice of x (GPU 0)     */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;

@@ -264,6 +264,7 @@ def test_config_c5_powerlaw_csr3_fp32():
     maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
     x = gen.rand_x(A.n, 9).astype(np.float32)
     y, info = gpu_spmv(A, x, maps)
+    assert info["x_slabs"] == 4  # random columns over an 8 MB x: 2 MB column slabs
     y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
     ok = short_rows(A)
     assert np.array_equal(y[ok].view(np.uint32), y32[ok].view(np.uint32))
@@ -468,3 +469,65 @@ def test_xdict_bitwise_and_fallback(monkeypatch):
     A = gen.stencil27(20)
     _, idef = gpu_spmv(A, gen.rand_x(A.n, 1))
     assert idef["x_dict"] == 0
+
+
+def _slab_exact_rows(A, slabs):
+    """Rows whose every x-slab segment has <= SERIAL_MAX nonzeros: the slab
+    passes sum them left to right from 0, i.e. bit-identical to omp_spmv."""
+    w = -(-A.n // slabs)
+    rows = np.repeat(np.arange(A.m), np.diff(A.row_ptr))
+    seg = np.zeros((A.m, slabs), np.int64)
+    np.add.at(seg, (rows, A.col_idx.astype(np.int64) // w), 1)
+    lens = np.diff(A.row_ptr)
+    return (seg.max(axis=1, initial=0) <= SERIAL_MAX) & (lens <= 4096)
+
+
+def test_xslabs_bitwise_rows_and_fallback(monkeypatch):
+    """x slabs (HSPMV_XSLABS=B forces B column slabs): the row kernel runs
+    once per slab over a slab-major copy, each pass continuing the rows
+    from y.  Rows whose slab segments are all <= 32 nonzeros are
+    bit-identical to the oracle (fp64 restatement, fp32 reference loop),
+    the rest within the fp64 bar; split rows, empty rows, CSR3 tasks,
+    prefetch and U = 2 included.  Unsorted rows fall back (x_slabs = 0)."""
+    cases = [_wide_random(3000, 1 << 20, 40, 4), gen.powerlaw(100000, seed=3, dtype=np.float64),
+             _split_row_matrix(), gen.laplace2d(1, 1), gen.laplace2d(300, 200)]
+    for A in cases:
+        for slabs in (2, 5):
+            monkeypatch.setenv("HSPMV_XSLABS", str(slabs))
+            exact = _slab_exact_rows(A, min(slabs, A.n))
+            for dt in (np.float64, np.float32):
+                Ad = A.astype(dt)
+                x = gen.rand_x(A.n, 9).astype(dt)
+                maps = hspmv.build_csr3_maps(Ad, 20, 10)
+                ref = oracle.spmv(Ad.row_ptr, Ad.col_idx, Ad.val, x)
+                for kw, mp in [(dict(kernel="stream"), None), (dict(kernel="csr3"), maps),
+                               (dict(kernel="stream", prefetch=True), None),
+                               (dict(kernel="stream", chunk_u=2, nontemporal=True), None)]:
+                    ys, info = gpu_spmv(Ad, x, mp, **kw)
+                    want = min(slabs, A.n) if min(slabs, A.n) >= 2 else 0
+                    assert info["x_slabs"] == want, (kw, info["x_slabs"])
+                    assert np.array_equal(ys[exact].view(np.uint8), ref[exact].view(np.uint8)), kw
+                    if dt == np.float64:
+                        check_fp64(Ad, x, ys)
+                    else:
+                        absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x.astype(np.float64))
+                        nrow = np.diff(A.row_ptr)
+                        err = np.abs(ys.astype(np.float64) - ref.astype(np.float64))
+                        assert np.all(err <= (nrow + 2) * 2.0 ** -23 * absrow + 1e-30), kw
+    # a row whose columns go back to an earlier slab: the slab passes would
+    # reorder its sum -> off (unsorted columns inside one slab are fine)
+    A = gen.laplace2d(50, 50)
+    ci = A.col_idx.copy()
+    ci[A.row_ptr[10]] = 2400  # row 10: [2400, 10, 11, 60] -> slabs 2, 0, 0, 0
+    Au = hspmv.CsrMatrix(A.m, A.n, A.row_ptr, ci, A.val)
+    monkeypatch.setenv("HSPMV_XSLABS", "3")
+    x = gen.rand_x(A.n, 2)
+    yu, iu = gpu_spmv(Au, x)
+    assert iu["x_slabs"] == 0
+    check_fp64(Au, x, yu, exact_rows=short_rows(Au))
+    # the vector kernel never uses slabs; default on small matrices: none
+    _, iv = gpu_spmv(A, x, kernel="vector")
+    assert iv["x_slabs"] == 0
+    monkeypatch.delenv("HSPMV_XSLABS")
+    _, idef = gpu_spmv(gen.powerlaw(100000, seed=3, dtype=np.float64), gen.rand_x(100000, 1))
+    assert idef["x_slabs"] == 0
