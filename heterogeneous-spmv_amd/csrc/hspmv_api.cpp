@@ -565,6 +565,11 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
   if (forced < 0) {
     const double footprint = (double)nnz * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv;
     if (footprint <= kMallResident || (double)n * sv <= 4.0 * 1024 * 1024) return HSPMV_OK;
+    // the passes must pay: every extra one re-reads a row-pointer array and
+    // y and rewrites y (at most a quarter of the matrix stream in total),
+    // and each pass must stream millions of nonzeros (a launch is ~2-5 us)
+    const double extra = (double)(B - 1) * (4.0 * (double)(m + 1) + 2.0 * sv * (double)m);
+    if (extra > 0.25 * (double)nnz * (sv + 4.0) || (double)nnz / B < 2.0e6) return HSPMV_OK;
     // irregular: the median 64-row group gathers over more than an L2 of x
     std::vector<int64_t> wide((size_t)nt, 0), nonempty((size_t)nt, 0);
     par([&](int t) {
@@ -651,6 +656,7 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
   if ((rc = build_xslabs(s, rp, col, val, m, n, dtype, flags))) return rc;
   if (s.n_slabs) {  // slab passes read 32-bit columns from global x
     s.A.col_span_bits = 31;
+    s.A.n_slabs = s.n_slabs;
     return HSPMV_OK;
   }
   s.h_xwin = xwin_table(rp, col, m, nullptr);

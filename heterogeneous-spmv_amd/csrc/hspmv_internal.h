@@ -24,6 +24,7 @@ struct DevCSR {
   const uint64_t *cplanes = nullptr;
   int32_t n_cplanes = 0, cplane_words = 0;
   int32_t col_span_bits = 0;  // bits of the widest 256-nonzero block's column span (0 = unknown)
+  int32_t n_slabs = 1;        // x slabs: the row kernel's passes (each sees ~nnz / n_slabs)
 };
 
 constexpr int kC16Shift = 8;  // 256 nonzeros per column-base block

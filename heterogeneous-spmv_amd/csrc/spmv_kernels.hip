@@ -221,7 +221,11 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   const unsigned k = flags & 0xFu;
   p.nontemporal = (flags & (1u << 12)) != 0;  // HSPMV_FLAG_NONTEMPORAL
   p.prefetch = (flags & (1u << 21)) != 0;  // HSPMV_FLAG_PREFETCH
-  const double d = A.m ? (double)A.nnz / (double)A.m : 0.0;
+  // (with x slabs each pass sees ~d / n_slabs per row, but the chunk size
+  // is still picked from d: U = 8 over U = 4/6 on C5's slab passes, 284 vs
+  // 320 us -- more gathers in flight per wave; profiles/r01_ab_c5_slabs_u.jsonl)
+  const double d_all = A.m ? (double)A.nnz / (double)A.m : 0.0;
+  const double d = d_all;
   // XCD block order: a contiguous eighth of the rows per XCD keeps x in that
   // XCD's L2, which pays when the matrix is served from the Infinity Cache;
   // from HBM the dispatch order (the whole chip on one compact window)
@@ -250,7 +254,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   switch (p.kernel) {
     case kVector: {
       int lanes = (int)((flags >> 4) & 0x7Fu);
-      if (lanes == 0) lanes = floor_pow2(d < 2.0 ? 2.0 : d);
+      if (lanes == 0) lanes = floor_pow2(d_all < 2.0 ? 2.0 : d_all);
       p.lanes = lanes;
       int64_t threads = (int64_t)A.m * lanes;
       int64_t blocks = (threads + 255) / 256;
