@@ -87,6 +87,38 @@ def stencil27(n: int, seed: int = 7, rcm: bool = True, dtype=np.float64) -> CsrM
     return CsrMatrix.from_scipy(S, dtype)
 
 
+def honeycomb(nx: int, ny: int, seed: int = 5, rcm: bool = True, dtype=np.float64) -> CsrMatrix:
+    """Brick-wall (honeycomb) lattice graph on nx x ny vertices: neighbours
+    (i +- 1, j) and (i, j + 1) when i + j is even, else (i, j - 1); degree
+    <= 3, no diagonal, values U(-1,1), RCM-permuted.  Stand-in for the
+    reference's DIMACS10 bubble meshes (helpers/overhead.txt:33-34,
+    hugebubbles-00000: 18,318,143 rows, 54,940,162 nnz, degree 3): at
+    nx = ny = 4280 it has 18.3 M rows and 54.9 M nonzeros."""
+    import scipy.sparse as sp
+    N = nx * ny
+    idx = np.arange(N, dtype=np.int64)
+    i, j = idx % nx, idx // nx
+    rows, cols = [], []
+    ok = i + 1 < nx
+    rows += [idx[ok], idx[ok] + 1]
+    cols += [idx[ok] + 1, idx[ok]]
+    ok = ((i + j) % 2 == 0) & (j + 1 < ny)
+    rows += [idx[ok], idx[ok] + nx]
+    cols += [idx[ok] + nx, idx[ok]]
+    r = np.concatenate(rows)
+    c = np.concatenate(cols)
+    del rows, cols, idx, i, j, ok
+    rng = np.random.default_rng(seed)
+    S = sp.csr_matrix((rng.uniform(-1.0, 1.0, r.shape[0]), (r, c)), shape=(N, N))
+    del r, c
+    if rcm:
+        from scipy.sparse.csgraph import reverse_cuthill_mckee
+        perm = reverse_cuthill_mckee(S, symmetric_mode=True)
+        S = S[perm][:, perm].tocsr()
+    S.sort_indices()
+    return CsrMatrix.from_scipy(S, dtype)
+
+
 def banded(m: int, per_row: int = 10, half: int = 32, seed: int = 11, r0: int = 0,
            r1: int | None = None, dtype=np.float64, chunk: int = 1 << 20) -> CsrMatrix:
     """Rows [r0, r1) of the C4 banded matrix: per_row distinct offsets per row

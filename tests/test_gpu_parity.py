@@ -244,6 +244,24 @@ def test_config_c3_stencil27_csr3_fp64():
     check_fp64(A, x, y, exact_rows=slice(None))
 
 
+def test_config_c3_alt_honeycomb_fp64():
+    """BASELINE configs[2]'s SuiteSparse example, hugebubbles-00000
+    (helpers/overhead.txt:33-34), has no copy here: its stand-in is an
+    RCM-ordered degree-3 honeycomb mesh of the same size (18.3 M rows,
+    54.9 M nnz).  Every row is <= 3 nonzeros, so y is bit-identical to the
+    oracle, through STREAM and through CSR-3 with the .csr3 writer's
+    grouping."""
+    A = gen.honeycomb(4280, 4280)
+    assert A.m == 18_318_400 and A.nnz == 54_942_360
+    x = gen.rand_x(A.n, 13)
+    y, info = gpu_spmv(A, x)
+    y64 = check_fp64(A, x, y, exact_rows=slice(None))
+    maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "volta"))
+    y3, i3 = gpu_spmv(A, x, maps)
+    assert i3["kernel_name"] == "csr3"
+    assert np.array_equal(y3, y64)
+
+
 def test_config_c4_banded_shard_fp64():
     """BASELINE configs[3]: one rank's row-range shard of the 2e7-row banded
     matrix (P = 8 -> 2.5 M rows), global columns, full-length x."""
