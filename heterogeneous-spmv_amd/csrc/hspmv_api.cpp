@@ -461,6 +461,14 @@ bool plan_xdict(const int32_t *rp, const int32_t *col, const std::vector<int32_t
 
 // Workgroup row ranges of the row kernel `kern` (STREAM: 256 rows; CSR3:
 // four packed tasks).
+// Packed CSR3 tasks per dictionary workgroup: 4, or 8 with HSPMV_XD_WAVES=8
+// (512 rows share one dictionary: fewer staged entries per row, half the
+// barriers, twice the LDS per block).
+int xd_task_waves() {
+  const char *e = getenv("HSPMV_XD_WAVES");
+  return (e && atoi(e) == 8) ? 8 : 4;
+}
+
 std::vector<int32_t> xdict_blocks(int kern, int64_t m, const std::vector<int32_t> &tasks) {
   std::vector<int32_t> bs;
   if (kern == kStream) {
@@ -468,7 +476,7 @@ std::vector<int32_t> xdict_blocks(int kern, int64_t m, const std::vector<int32_t
     bs.push_back((int32_t)m);
   } else {
     const int64_t nt = (int64_t)tasks.size() - 1;
-    for (int64_t t = 0; t < nt; t += 4) bs.push_back(tasks[(size_t)t]);
+    for (int64_t t = 0; t < nt; t += xd_task_waves()) bs.push_back(tasks[(size_t)t]);
     bs.push_back(tasks[(size_t)nt]);
   }
   return bs;
@@ -517,6 +525,7 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
   s.A.cplanes = nullptr;
   s.A.n_cplanes = 0;
   s.xd_shape = kern;
+  if (kern == kCsr3) s.A.task_waves = xd_task_waves();
   s.xd_lds_bytes = (int32_t)((int64_t)P.tmax * (int64_t)sv);
   s.xd_entries = P.entries;
   s.xd_runs_n = (int64_t)P.rec.size() / 2;
@@ -784,7 +793,7 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
   if (s.xd_shape) {
     const bool fits = (s.xd_shape == kStream && s.plan.kernel == kStream && s.plan.groups == 1) ||
                       (s.xd_shape == kCsr3 && s.plan.kernel == kCsr3 && !s.h_tasks.empty() &&
-                       s.plan.waves_per_block == 4);
+                       s.plan.waves_per_block == s.A.task_waves);
     if (fits) {
       s.dp.xd_blk = s.d_xd_blk;
       s.dp.xd_runs = s.d_xd_runs;

@@ -25,6 +25,7 @@ struct DevCSR {
   int32_t n_cplanes = 0, cplane_words = 0;
   int32_t col_span_bits = 0;  // bits of the widest 256-nonzero block's column span (0 = unknown)
   int32_t n_slabs = 1;        // x slabs: the row kernel's passes (each sees ~nnz / n_slabs)
+  int32_t task_waves = 4;     // CSR3 packed tasks per workgroup (4, or 8 with x dictionaries)
 };
 
 constexpr int kC16Shift = 8;  // 256 nonzeros per column-base block

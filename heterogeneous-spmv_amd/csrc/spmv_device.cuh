@@ -547,8 +547,11 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C, W, XW, X>), dim3((unsigned)p.blocks),      \
                      dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,     \
                      (int32_t)p.y_nt, p.carry, dp.task_start, xw, xd, A.row_ptr, cs, val, x, y)
-  if constexpr (XD) {  // packed tasks only (4 per block)
-    HSPMV_CSR3(4, false, false, true);
+  if constexpr (XD) {  // packed tasks only (4 or 8 per block)
+    if (p.waves_per_block == 8)
+      HSPMV_CSR3(8, false, false, true);
+    else
+      HSPMV_CSR3(4, false, false, true);
     return;
   } else {
     if (xw && p.waves_per_block == 4) {  // x windows: packed tasks only (4 per block)
@@ -597,7 +600,7 @@ hipError_t launch_rows(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, 
                        hipStream_t st) {
   if (dp.xd_blk) {
     if (!A.col16 || (p.kernel == kStream && p.groups != 1) ||
-        (p.kernel == kCsr3 && (!dp.task_start || p.waves_per_block != 4)))
+        (p.kernel == kCsr3 && (!dp.task_start || (p.waves_per_block != 4 && p.waves_per_block != 8))))
       return hipErrorInvalidValue;  // the host built the dictionary for another block shape
     return launch_rows_c<T, false, true>(A, dp, p, x, y, st);
   }

@@ -275,12 +275,12 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
     }
     case kCsr3: {
       p.lanes = kWave;
-      if (packed_tasks > 0) {  // super-rows packed into <= 64-row tasks, 4 per block
-        p.waves_per_block = 4;
+      if (packed_tasks > 0) {  // super-rows packed into <= 64-row tasks, 4 (or 8) per block
+        p.waves_per_block = A.task_waves == 8 ? 8 : 4;
         const double rows_per_task = (double)A.m / (double)packed_tasks;
         const double per_pass = (rows_per_task < 64.0 ? rows_per_task : 64.0) * d;
         p.u = forced_u ? forced_u : pick_u(per_pass < 64.0 * kLongRow ? per_pass : 64.0 * kLongRow, dtype);
-        p.blocks = (packed_tasks + 3) / 4;
+        p.blocks = (packed_tasks + p.waves_per_block - 1) / p.waves_per_block;
         break;
       }
       // ~64 rows per wave (one lane per row in the ordered sums)
