@@ -246,6 +246,79 @@ int build_col16(Shard &s, const int32_t *col, int64_t nnz, int64_t m, int64_t n,
   return HSPMV_OK;
 }
 
+// Group-base 16-bit column offsets (STREAM): when every 64-row group's
+// columns span < 65536, col = base[g] + off16 with one int32 base per
+// group -- 2 instead of 4 index bytes per nonzero for one scalar load per
+// group and one add per element, none of the per-256-nonzero base pairs,
+// selects and planes of build_col16.  Auto: Infinity-Cache-resident
+// matrices (C2: 15.56 -> 15.12 us in one process, bench 724-732 -> 754
+// GFLOP/s); HBM-resident ones keep build_col16's blocks (C4 53.0 vs 55.4
+// us with group bases, c3h/l4k within 1 %; profiles/r01_ab_col16_group*.jsonl).
+// HSPMV_COL16G=0 disables, =1 uses it whenever it fits.  Split rows (read
+// by the split-row kernels from the 32-bit columns) get offset 0.
+int build_col16g(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int64_t n, int dtype,
+                 unsigned flags, bool *used) {
+  *used = false;
+  const char *env = getenv("HSPMV_COL16G");
+  const int mode = env ? atoi(env) : -1;  // -1 auto, 0 off, 1 on whenever it fits
+  const int64_t nnz = rp[m];
+  if (mode == 0 || (flags & HSPMV_FLAG_NO_COL16) || nnz == 0) return HSPMV_OK;
+  const double sv = (double)dtype_size(dtype);
+  const bool forced = (flags & HSPMV_FLAG_COL16) != 0 || mode == 1;
+  if (!forced && (double)nnz * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv > kMallResident)
+    return HSPMV_OK;
+  const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
+  const int64_t ng = (m + 63) / 64;
+  std::vector<int32_t> base((size_t)ng + 1, 0);  // +1: read by 8-byte scalar loads
+  std::vector<int32_t> span((size_t)ng, 0);
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, ng / 4096));
+  auto par = [&](auto &&body) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back([&, t]() { body(ng * t / nt, ng * (t + 1) / nt); });
+    for (auto &x : th) x.join();
+  };
+  par([&](int64_t g0, int64_t g1) {
+    for (int64_t g = g0; g < g1; ++g) {
+      int32_t lo = INT32_MAX, hi = -1;
+      for (int64_t r = 64 * g; r < std::min(m, 64 * g + 64); ++r) {
+        if (rp[r + 1] - rp[r] > long_t) continue;
+        for (int32_t k = rp[r]; k < rp[r + 1]; ++k) {
+          lo = std::min(lo, col[k]);
+          hi = std::max(hi, col[k]);
+        }
+      }
+      base[(size_t)g] = hi >= 0 ? lo : 0;
+      span[(size_t)g] = hi >= 0 ? hi - lo : 0;
+    }
+  });
+  int32_t maxspan = 0;
+  for (int32_t v : span) maxspan = std::max(maxspan, v);
+  if (maxspan > 65535) return HSPMV_OK;
+  std::vector<uint16_t> off((size_t)nnz, 0);
+  par([&](int64_t g0, int64_t g1) {
+    for (int64_t g = g0; g < g1; ++g)
+      for (int64_t r = 64 * g; r < std::min(m, 64 * g + 64); ++r) {
+        if (rp[r + 1] - rp[r] > long_t) continue;
+        for (int32_t k = rp[r]; k < rp[r + 1]; ++k) off[(size_t)k] = (uint16_t)(col[k] - base[(size_t)g]);
+      }
+  });
+  int rc;
+  if ((rc = dev_alloc(&s.d_c16, 2 * (size_t)nnz, &s.bytes))) return rc;
+  if ((rc = dev_alloc(&s.d_cbase, 4 * base.size(), &s.bytes))) return rc;
+  HIP_TRY(hipMemcpy(s.d_c16, off.data(), 2 * (size_t)nnz, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s.d_cbase, base.data(), 4 * base.size(), hipMemcpyHostToDevice));
+  int bits = 0;
+  while (bits < 31 && (int64_t(1) << bits) <= maxspan) ++bits;
+  s.A.col_span_bits = std::max(1, bits);
+  s.A.col16 = s.d_c16;
+  s.A.cbase = s.d_cbase;
+  s.A.cplanes = nullptr;
+  s.A.n_cplanes = 0;
+  s.A.c16_mode = 2;
+  *used = true;
+  return HSPMV_OK;
+}
+
 // x windows of the STREAM kernel's 64-row groups: {lo, w} with w = the
 // group's column span when it is at most kXWin entries (its x slice is then
 // staged in LDS and gathered from there), else 0.  Kept only when at least
@@ -681,7 +754,8 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
     return HSPMV_OK;
   }
   bool c16 = false;
-  if ((rc = build_col16(s, col, rp[m], m, n, dtype, flags, &c16))) return rc;
+  if (kern == kStream && (rc = build_col16g(s, rp, col, m, n, dtype, flags, &c16))) return rc;
+  if (!c16 && (rc = build_col16(s, col, rp[m], m, n, dtype, flags, &c16))) return rc;
   return HSPMV_OK;
 }
 
@@ -806,6 +880,11 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     } else {  // planned for another block shape: the kernels read the 32-bit columns
       s.A.col16 = nullptr;
     }
+  } else if (s.A.col16 && s.A.c16_mode == 2 && s.plan.kernel != kStream) {
+    s.A.col16 = nullptr;  // group bases were built for STREAM's groups: 32-bit columns
+    s.A.cbase = nullptr;
+  } else if (s.A.col16 && s.A.c16_mode == 2) {
+    s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)((s.A.m + 63) / 64);
   } else if (s.A.col16) {
     const int64_t nb = (s.A.nnz + (int64_t(1) << kC16Shift) - 1) >> kC16Shift;
     s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)nb -
@@ -1292,6 +1371,7 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->x_windows = s.dp.xwin ? 1 : 0;
   out->x_dict = s.dp.xd_blk ? 1 : 0;
   out->x_slabs = s.dp.n_slabs;
+  out->col16_group = (s.A.col16 && s.A.c16_mode == 2) ? 1 : 0;
   for (auto &sh : h->shards) out->x_dict_entries += sh.dp.xd_blk ? sh.xd_entries : 0;
   return HSPMV_OK;
 }

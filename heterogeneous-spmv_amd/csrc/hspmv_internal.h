@@ -23,6 +23,9 @@ struct DevCSR {
   const int32_t *cbase = nullptr;
   const uint64_t *cplanes = nullptr;
   int32_t n_cplanes = 0, cplane_words = 0;
+  // c16_mode 2 (STREAM only): col[k] = cbase[g] + col16[k] with g = the
+  // nonzero's 64-row group, when every group's columns span < 65536
+  int32_t c16_mode = 1;
   int32_t col_span_bits = 0;  // bits of the widest 256-nonzero block's column span (0 = unknown)
   int32_t n_slabs = 1;        // x slabs: the row kernel's passes (each sees ~nnz / n_slabs)
   int32_t task_waves = 4;     // CSR3 packed tasks per workgroup (4, or 8 with x dictionaries)

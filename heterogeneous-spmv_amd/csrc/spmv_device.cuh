@@ -174,14 +174,14 @@ struct XWin {
 // C forms the products into LDS; then the row sums.  PF (software
 // pipelining): the next chunk's stage A is issued between this chunk's
 // stage B and C, so its latency overlaps the gather and the sums.
-template <typename T, bool NT, int U, bool PF, bool C16, bool XW, bool XD>
+template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD>
 __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, int32_t end,
                                           int32_t long_t, const ColSrc &cs,
                                           const T *__restrict__ val,
                                           const T *__restrict__ x,
                                           T *__restrict__ y, T *lds, int lane,
                                           const XWin<T> &win, bool y_nt, bool carry,
-                                          unsigned long long *ts = nullptr) {
+                                          int32_t gbase, unsigned long long *ts = nullptr) {
   const int32_t row = g0 + lane;
   const bool valid = row < g1;
   const int32_t len = end - beg;
@@ -221,7 +221,11 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
           const uint32_t j = (uint32_t)(c0 + min(u * kWave + lane, last));
           if constexpr (XD) {
             col[u] = (int32_t)ld_off<NT, uint16_t>(cb, j * 2u);  // position in the block's xs
-          } else if constexpr (C16) {
+          } else if constexpr (C16 == 2) {
+            // group-base offsets: col = the 64-row group's smallest column
+            // + 16-bit offset (one scalar load per group, one add here)
+            col[u] = gbase + (int32_t)ld_off<NT, uint16_t>(cb, j * 2u);
+          } else if constexpr (C16 == 1) {
             // col = base of the nonzero's 256-block + 16-bit offset.  The 64
             // lanes of a slice lie in at most two consecutive blocks: one
             // scalar load brings both bases (s_load, no vector memory op)
@@ -397,7 +401,7 @@ __device__ __forceinline__ void stage_xdict(T *xs, const T *__restrict__ x, cons
 // w * groups * 64, loading the next group's row pointers before streaming
 // the current one.  XW: groups whose x window (xwin[g] = {lo, w}) fits
 // kXWin entries gather from an LDS copy of it.
-template <typename T, bool NT, int U, bool PF, bool C16, bool XW, bool XD>
+template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD>
 __global__ __launch_bounds__(256) void hspmv_csr_stream(
     int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups, int32_t y_nt, int32_t carry,
     const int32_t *__restrict__ rp, ColSrc cs, const int2 *__restrict__ xwin, XDict xd,
@@ -443,8 +447,10 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
     }
     int32_t nbeg = 0, nend = 0;
     if (g1 < gend) group_bounds(rp, g1, (int32_t)min<int64_t>(g1 + kWave, gend), lane, nbeg, nend);
+    int32_t gbase = 0;
+    if constexpr (C16 == 2) gbase = (int32_t)sload_i64(cs.cbase, (uint64_t)(g0 / kWave) * 4u);
     wave_rows<T, NT, U, PF, C16, XW, XD>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my,
-                                         lane, win, y_nt != 0, carry != 0, ts);
+                                         lane, win, y_nt != 0, carry != 0, gbase, ts);
     ts = nullptr;  // trace the first group only
     if (g1 >= gend) break;
     g0 = g1;
@@ -453,7 +459,7 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
   }
 }
 
-template <typename T, bool NT, int U, bool PF, bool C16, int W, bool XW, bool XD>
+template <typename T, bool NT, int U, bool PF, int C16, int W, bool XW, bool XD>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, int32_t y_nt, int32_t carry,
     const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin, XDict xd,
@@ -502,7 +508,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
     wave_rows<T, NT, U, PF, C16, XW, XD>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                         win, y_nt != 0, carry != 0, ts);
+                                         win, y_nt != 0, carry != 0, 0, ts);
     ts = nullptr;
     beg = nbeg;
     end = nend;
@@ -515,7 +521,7 @@ inline ColSrc col_src(const DevCSR &A) {
   return ColSrc{A.col_idx, A.col16, A.cbase, A.cplanes, A.n_cplanes, A.cplane_words};
 }
 
-template <typename T, bool NT, int U, bool PF, bool C16, bool XD>
+template <typename T, bool NT, int U, bool PF, int C16, bool XD>
 void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x, T *y,
                    hipStream_t st) {
   const T *val = static_cast<const T *>(A.val);
@@ -542,6 +548,9 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
                          xw, xd, val, x, y);
     return;
   }
+  if constexpr (C16 == 2) {
+    return;  // group-base offsets are built for STREAM's groups only (launch_rows checks)
+  } else {
   const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
 #define HSPMV_CSR3(W, C, XW, X)                                                               \
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C, W, XW, X>), dim3((unsigned)p.blocks),      \
@@ -566,9 +575,10 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
     }
   }
 #undef HSPMV_CSR3
+  }
 }
 
-template <typename T, bool NT, bool PF, bool C16, bool XD>
+template <typename T, bool NT, bool PF, int C16, bool XD>
 hipError_t launch_rows_pf(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x,
                           T *y, hipStream_t st) {
   switch (p.u) {
@@ -583,7 +593,7 @@ hipError_t launch_rows_pf(const DevCSR &A, const DevPlan &dp, const LaunchPlan &
   return hipGetLastError();
 }
 
-template <typename T, bool C16, bool XD>
+template <typename T, int C16, bool XD>
 hipError_t launch_rows_c(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, const T *x,
                          T *y, hipStream_t st) {
   if (p.nontemporal)
@@ -602,10 +612,14 @@ hipError_t launch_rows(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, 
     if (!A.col16 || (p.kernel == kStream && p.groups != 1) ||
         (p.kernel == kCsr3 && (!dp.task_start || (p.waves_per_block != 4 && p.waves_per_block != 8))))
       return hipErrorInvalidValue;  // the host built the dictionary for another block shape
-    return launch_rows_c<T, false, true>(A, dp, p, x, y, st);
+    return launch_rows_c<T, 0, true>(A, dp, p, x, y, st);
   }
-  return A.col16 ? launch_rows_c<T, true, false>(A, dp, p, x, y, st)
-                 : launch_rows_c<T, false, false>(A, dp, p, x, y, st);
+  if (A.col16 && A.c16_mode == 2) {
+    if (p.kernel != kStream) return hipErrorInvalidValue;  // built for STREAM's groups
+    return launch_rows_c<T, 2, false>(A, dp, p, x, y, st);
+  }
+  return A.col16 ? launch_rows_c<T, 1, false>(A, dp, p, x, y, st)
+                 : launch_rows_c<T, 0, false>(A, dp, p, x, y, st);
 }
 
 }  // namespace dev

@@ -111,7 +111,8 @@ class Info(C.Structure):
                 ("n_split_rows", C.c_int32), ("xcd_remap", C.c_int32), ("groups_per_wave", C.c_int32),
                 ("x_entries", C.c_int64), ("format_bytes", C.c_double), ("col16", C.c_int32),
                 ("wave_tasks", C.c_int32), ("x_windows", C.c_int32), ("x_dict", C.c_int32),
-                ("x_dict_entries", C.c_int64), ("x_slabs", C.c_int32)]
+                ("x_dict_entries", C.c_int64), ("x_slabs", C.c_int32),
+                ("col16_group", C.c_int32)]
 
 
 _P = C.c_void_p

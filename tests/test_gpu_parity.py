@@ -398,35 +398,49 @@ def _band_random(m, per_row, half, seed):
                            rng.uniform(-1, 1, m * per_row))
 
 
-def test_col16_offsets_bitwise_and_fallback():
-    """16-bit column offsets (+ p high-bit planes; forced here, p <= 8) give
-    the same y bit for bit as 32-bit columns, through STREAM, CSR3, prefetch
-    and split rows; p grows with the column span of a 256-nonzero block, and
-    a matrix needing more than 8 planes keeps 32-bit columns.  By default
-    these small (Infinity-Cache-resident) matrices keep 32-bit columns."""
-    cases = [(gen.laplace2d(300, 200), 1),                        # spans < 65536
-             (gen.stencil27(20), 1),
-             (gen.banded(30000, per_row=10, half=32, seed=5), 1),
-             (_band_random(150000, 10, 50000, 6), 2),               # 1 plane
-             (gen.powerlaw(200000, seed=3, dtype=np.float64), 3),     # 2 planes
-             (_split_row_matrix(), None),
-             (_wide_random(2000, 1 << 25, 40, 4), 0)]                 # 10 planes: off
-    for A, want in cases:
+def test_col16_offsets_bitwise_and_fallback(monkeypatch):
+    """16-bit column offsets give the same y bit for bit as 32-bit columns,
+    through STREAM, CSR3, prefetch and split rows, in both encodings:
+    per-256-nonzero block bases + p high-bit planes (forced here with
+    HSPMV_COL16G=0, p <= 8; p grows with a block's column span and a matrix
+    needing more than 8 planes keeps 32-bit columns), and one base per
+    64-row STREAM group (HSPMV_COL16G=1) when every group spans < 65536.
+    By default these small (Infinity-Cache-resident) matrices use the group
+    bases where they fit and 32-bit columns otherwise."""
+    cases = [(gen.laplace2d(300, 200), 1, True),                  # spans < 65536
+             (gen.stencil27(20), 1, True),
+             (gen.banded(30000, per_row=10, half=32, seed=5), 1, True),
+             (_band_random(150000, 10, 50000, 6), 2, False),          # 1 plane
+             (gen.powerlaw(200000, seed=3, dtype=np.float64), 3, False),  # 2 planes
+             (_split_row_matrix(), None, False),
+             (_wide_random(2000, 1 << 25, 40, 4), 0, False)]            # 10 planes: off
+    for A, want, group_fits in cases:
         x = gen.rand_x(A.n, 9)
         maps = hspmv.build_csr3_maps(A, 20, 10)
         for kw, mp in [(dict(kernel="stream"), None), (dict(kernel="stream", prefetch=True), None),
                        (dict(kernel="csr3"), maps), (dict(kernel="stream", chunk_u=2), None)]:
+            monkeypatch.setenv("HSPMV_COL16G", "0")
             y16, i16 = gpu_spmv(A, x, mp, col16=True, **kw)
+            monkeypatch.setenv("HSPMV_COL16G", "1")
+            y16g, i16g = gpu_spmv(A, x, mp, col16=True, **kw)
             y32, i32 = gpu_spmv(A, x, mp, col16=False, **kw)
             assert i32["col16"] == 0 and i32["format_bytes"] == i32["alg_bytes"]
+            assert i16["col16_group"] == 0
             if want is not None:
                 assert i16["col16"] == want, (kw, i16["col16"], want)
             if i16["col16"]:
                 assert i16["format_bytes"] < i16["alg_bytes"]
+            g = group_fits and kw["kernel"] == "stream"
+            assert i16g["col16_group"] == int(g), (kw, i16g["col16_group"])
+            if g:
+                assert i16g["col16"] == 1 and i16g["format_bytes"] < i16g["alg_bytes"]
             assert np.array_equal(y16, y32), kw
+            assert np.array_equal(y16g, y32), kw
         check_fp64(A, x, y16, exact_rows=short_rows(A))
+        monkeypatch.delenv("HSPMV_COL16G")
         _, idef = gpu_spmv(A, x)
-        assert idef["col16"] == 0  # small: default keeps 32-bit columns
+        assert idef["col16_group"] == int(group_fits)
+        assert idef["col16"] == int(group_fits)  # small: block offsets only when forced
     # the vector kernel always reads 32-bit columns
     A = gen.laplace2d(100, 100)
     _, iv = gpu_spmv(A, gen.rand_x(A.n, 1), kernel="vector", col16=True)
