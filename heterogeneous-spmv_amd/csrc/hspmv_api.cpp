@@ -1064,9 +1064,12 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
       s.mean_rows_per_ssr = (double)A->m / (double)maps->n_ssr;
       h->n_ssr = maps->n_ssr; h->n_sr = maps->n_sr;
     }
-    // (device values are not copied back: no x slabs for borrowed matrices)
-    if ((rc = build_row_tables(s, rp.data(), cols.data(), nullptr, A->m, A->n, A->dtype, flags)))
+    // the values come back to the host too: the x slabs copy them slab-major
+    std::vector<char> vals(dtype_size(A->dtype) * (size_t)A->nnz);
+    if (A->nnz) HIP_TRY(hipMemcpy(vals.data(), A->val, vals.size(), hipMemcpyDeviceToHost));
+    if ((rc = build_row_tables(s, rp.data(), cols.data(), vals.data(), A->m, A->n, A->dtype, flags)))
       return rc;
+    std::vector<char>().swap(vals);
     std::vector<int32_t>().swap(cols);
     const size_t sv = dtype_size(A->dtype);
     if ((rc = dev_alloc(&s.d_x, sv * (size_t)A->n, &s.bytes))) return rc;

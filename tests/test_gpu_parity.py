@@ -354,9 +354,11 @@ def test_chunk_u_and_remap_variants():
             assert fp64_tol_ok(y, y64, absrow)
 
 
-def test_borrowed_device_arrays():
+def test_borrowed_device_arrays(monkeypatch):
     """HSPMV_FLAG_DEVICE_PTRS: the handle reads caller-owned device arrays
-    (torch tensors here) and caller-bound x / y."""
+    (torch tensors here) and caller-bound x / y; the host tables (x slabs
+    included: the values are read back for the slab-major copy) are built
+    from device reads."""
     import torch
     A = gen.stencil27(30)
     maps = hspmv.build_csr3_maps(A, 20, 10)
@@ -375,6 +377,18 @@ def test_borrowed_device_arrays():
         op.synchronize()
         check_fp64(A, x, yd.cpu().numpy(), exact_rows=short_rows(A) if kernel != "vector" else None)
         op.close()
+    monkeypatch.setenv("HSPMV_XSLABS", "3")
+    for mdev, kernel in ((None, "stream"), (ms, "csr3")):
+        yd.zero_()
+        op = hspmv.SpMV.from_device(cs, mdev, A, device=0, kernel=kernel)
+        assert op.info["x_slabs"] == 3
+        op.bind_x_device(xd.data_ptr())
+        op.bind_y_device(yd.data_ptr())
+        op.spmv()
+        op.synchronize()
+        check_fp64(A, x, yd.cpu().numpy(), exact_rows=short_rows(A))
+        op.close()
+    monkeypatch.delenv("HSPMV_XSLABS")
     bad = hspmv._lib.Csr(A.m, A.n, A.nnz, rp.data_ptr(), 0, val.data_ptr(), 1)
     with pytest.raises(hspmv.HspmvError, match="E_INVALID"):
         hspmv.SpMV.from_device(bad, None, A, device=0)
