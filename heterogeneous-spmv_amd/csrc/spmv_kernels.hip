@@ -204,13 +204,18 @@ int floor_pow2(double v) {
 // Elements per lane per LDS chunk.  Measured on MI355X (profiles/r01_sweep*):
 // the chunk must stay small enough for 8 waves/SIMD (U = 4: 62 VGPRs fp64),
 // and a 64-row group that fits one chunk of U <= 6 should be done in one.
-int pick_u(double nnz_per_pass, int dtype) {
+// fp32 (profiles/r01_ab_f32_u.jsonl): two chunks of U = 6 beat U = 8 on C4's
+// 640-nonzero groups (34.3 vs 40.2 us), and long groups take U = 16 (C3's
+// 27-point rows: 62.3 vs 67.4 us) -- except on x-slab passes, where U = 8
+// measured best (C5: 273 vs 291 us, r01_ab_c5_slabs_u.jsonl).
+int pick_u(double nnz_per_pass, int dtype, bool slabs) {
   if (nnz_per_pass <= 128.0) return 2;
   if (nnz_per_pass <= 192.0) return 3;
   if (nnz_per_pass <= 256.0) return 4;
   if (nnz_per_pass <= 384.0) return 6;
-  if (dtype == 1 && nnz_per_pass <= 768.0) return 6;  // two chunks (C4: -1.5 %, r01_ab_col16)
-  return dtype == 1 ? 4 : 8;
+  if (nnz_per_pass <= 768.0) return 6;  // two chunks (C4 fp64: -1.5 %, r01_ab_col16)
+  if (dtype == 1) return 4;
+  return slabs ? 8 : 16;
 }
 
 }  // namespace
@@ -265,7 +270,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
     }
     case kStream: {
       p.lanes = kWave;
-      p.u = forced_u ? forced_u : pick_u(64.0 * (d < kLongRow ? d : kLongRow), dtype);
+      p.u = forced_u ? forced_u : pick_u(64.0 * (d < kLongRow ? d : kLongRow), dtype, A.n_slabs > 1);
       const int64_t tasks = ((int64_t)A.m + kWave - 1) / kWave;
       const unsigned gcode = (flags >> 29) & 0x7u;  // HSPMV_GROUPS(g)
       p.groups = gcode ? 1 << (gcode - 1) : 1;
@@ -279,7 +284,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
         p.waves_per_block = A.task_waves == 8 ? 8 : 4;
         const double rows_per_task = (double)A.m / (double)packed_tasks;
         const double per_pass = (rows_per_task < 64.0 ? rows_per_task : 64.0) * d;
-        p.u = forced_u ? forced_u : pick_u(per_pass < 64.0 * kLongRow ? per_pass : 64.0 * kLongRow, dtype);
+        p.u = forced_u ? forced_u : pick_u(per_pass < 64.0 * kLongRow ? per_pass : 64.0 * kLongRow, dtype, A.n_slabs > 1);
         p.blocks = (packed_tasks + p.waves_per_block - 1) / p.waves_per_block;
         break;
       }
@@ -288,7 +293,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
       p.waves_per_block = w >= 6.0 ? 8 : (w >= 3.0 ? 4 : (w >= 1.5 ? 2 : 1));
       const double rows_per_task = rows_per_ssr / p.waves_per_block;
       const double per_pass = (rows_per_task < 64.0 ? rows_per_task : 64.0) * d;
-      p.u = forced_u ? forced_u : pick_u(per_pass < 64.0 * kLongRow ? per_pass : 64.0 * kLongRow, dtype);
+      p.u = forced_u ? forced_u : pick_u(per_pass < 64.0 * kLongRow ? per_pass : 64.0 * kLongRow, dtype, A.n_slabs > 1);
       p.blocks = A.n_ssr;
       break;
     }

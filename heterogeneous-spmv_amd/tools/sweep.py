@@ -37,6 +37,9 @@ PEAK = 8000.0
 
 
 def build(cfg):
+    if cfg.endswith(":f32"):  # any config in fp32 (the reference's own dtype)
+        A, maps, desc = build(cfg[:-4])
+        return A.astype(np.float32), maps, desc + " [fp32]"
     if cfg == "c2":
         A = gen.laplace2d(1000, 1000)
         return A, None, "C2 5-pt Laplacian 1000^2 CSR fp64"
