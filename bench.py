@@ -23,7 +23,8 @@ Extra fields on the line:
                2 nnz / (step + y all-gather), and the iterative form
                2 nnz / (step + halo exchange) where x is distributed like y
   cpu_baseline the oracle's OpenMP restatement of spmv-csr's omp_spmv on the
-               host cores, rank 0 at N = 1 only (bounded sample)
+               host cores, rank 0 at N = 1 only (bounded sample); beside it,
+               reference_f32: the reference's own spmv-csr program (fp32)
 """
 from __future__ import annotations
 
@@ -148,6 +149,49 @@ def cpu_baseline(A, x, budget_s: float):
                        "time_avg_s": g[2], "runs": g[4]}}
 
 
+def reference_cpu(A, runs: int = 200):
+    """The reference's own spmv-csr program (spmv-csr/spmv.c main, built
+    unmodified from /root/reference into oracle/_ref by oracle/Makefile) on
+    the fp32 version of the workload, run in a child process exactly as
+    `spmv.exe file.csr runs`: its reader, x = 1, `runs` serial test_spmv
+    calls, 5 warm-ups and `runs` timed omp_spmv calls (OMP_SCHEDULE=static,
+    run_norm.py:18).  Returns its TimeMin/TimeAvg, or None when the library
+    was not built (no /root/reference where build() ran)."""
+    import subprocess
+    import tempfile
+    lib = REPO / "oracle" / "_ref" / "libref_spmvcsr.so"
+    if not lib.exists():
+        return None
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "c2.mtx.rcm.csr")
+        hspmv.write_csr(path, A.astype(np.float32))  # the reference's text format (A15)
+        code = ("import ctypes, sys; L = ctypes.CDLL(sys.argv[1]); "
+                "a = (ctypes.c_char_p * 3)(b'spmv.exe', sys.argv[2].encode(), sys.argv[3].encode()); "
+                "L.ref_main(3, a)")
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_SCHEDULE="static")
+        try:
+            out = subprocess.run([sys.executable, "-c", code, str(lib), path, str(runs)], env=env,
+                                 capture_output=True, text=True, timeout=180)
+        except subprocess.TimeoutExpired:
+            return None
+    vals = {}
+    for line in out.stdout.splitlines():  # parsed like run_norm.py:94-107
+        for key in ("TimeMin:", "TimeMax:", "TimeAvg:"):
+            if line.startswith(key):
+                vals[key[:-1]] = float(line[len(key):].strip())
+    if out.returncode != 0 or "TimeAvg" not in vals:
+        return None
+    return {"kind": "reference", "dtype": "f32", "cores": threads,
+            "value": round(2.0 * A.nnz / vals["TimeAvg"] * 1e-9, 3), "unit": "GFLOP/s",
+            "gflops_from_min": round(2.0 * A.nnz / vals["TimeMin"] * 1e-9, 3),
+            "time_min_s": vals["TimeMin"], "time_avg_s": vals["TimeAvg"],
+            "time_max_s": vals.get("TimeMax"),
+            "sample": (f"the reference's spmv-csr main (oracle/_ref, built from spmv-csr/spmv.c) on "
+                       f"the C2 matrix in fp32 (its only dtype), x = 1, num_runs = {runs}, "
+                       f"OMP_SCHEDULE=static")}
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup(args)
@@ -258,6 +302,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(A, x.cpu().numpy(), args.cpu_seconds)
+        cpu["reference_f32"] = reference_cpu(A)
 
     if rank == 0:
         out = {

@@ -33,4 +33,7 @@ def test_bench_json_line_contract():
     assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
+    ref = c["reference_f32"]  # the reference's own program, when oracle/_ref was built
+    if (REPO / "oracle" / "_ref" / "libref_spmvcsr.so").exists():
+        assert ref["kind"] == "reference" and ref["value"] > 0 and ref["time_avg_s"] > 0
     assert d["check"]["pass"] is True
