@@ -202,6 +202,16 @@ def ref() -> C.CDLL:
     return _ref
 
 
+def ref_spmv(row_ptr, col_idx, val, x) -> np.ndarray:
+    """The reference's own omp_spmv (spmv-csr/spmv.c:92-114) on in-memory fp32
+    arrays (its reader is pinned separately by the golden fixtures)."""
+    R = ref()
+    rp, ci, v, xx = _prep(row_ptr, col_idx, np.asarray(val, np.float32), x)
+    y = np.zeros(rp.shape[0] - 1, np.float32)
+    R.omp_spmv(rp.shape[0] - 1, xx.shape[0], ci.shape[0], _c(rp), _c(ci), _c(v), _c(xx), _c(y))
+    return y
+
+
 def ref_spmv_file(path, x: np.ndarray | None = None, serial: bool = False) -> np.ndarray:
     """Runs the reference reader + omp_spmv (or test_spmv) on a .csr file.
     x defaults to all-ones (spmv-csr/spmv.c:133); otherwise float32(x)."""

@@ -577,3 +577,30 @@ def test_xslabs_bitwise_rows_and_fallback(monkeypatch):
     monkeypatch.delenv("HSPMV_XSLABS")
     _, idef = gpu_spmv(gen.powerlaw(100000, seed=3, dtype=np.float64), gen.rand_x(100000, 1))
     assert idef["x_slabs"] == 0
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c3h", "c4"])
+def test_full_size_fp32_bitwise_vs_reference_omp_spmv(cfg):
+    """BASELINE's configs at full size in fp32 -- the reference's only dtype --
+    against the reference's OWN omp_spmv (spmv-csr/spmv.c, built unmodified
+    into oracle/_ref): every row has <= 32 nonzeros, so the GPU's y must be
+    bit-identical (C3 through its CSR-3 maps)."""
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built (no /root/reference where build() ran)")
+    from hspmv import dist as hdist
+    if cfg == "c2":
+        A, maps = gen.laplace2d(1000, 1000), None
+    elif cfg == "c3":
+        A = gen.stencil27(125)
+        maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "volta"))
+    elif cfg == "c3h":
+        A, maps = gen.honeycomb(4280, 4280), None
+    else:
+        A, maps = hdist.build_shard("c4", 3, 8).A, None
+    A = A.astype(np.float32)
+    assert np.diff(A.row_ptr).max() <= SERIAL_MAX
+    x = gen.rand_x(A.n, 21).astype(np.float32)
+    y_ref = oracle.ref_spmv(A.row_ptr, A.col_idx, A.val, x)
+    y, info = gpu_spmv(A, x, maps)
+    assert info["kernel_name"] == ("csr3" if maps is not None else "stream")
+    assert np.array_equal(y.view(np.uint32), y_ref.view(np.uint32))
