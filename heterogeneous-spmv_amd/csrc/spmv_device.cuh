@@ -122,8 +122,11 @@ __device__ __forceinline__ int64_t sload_i64(const void *p, uint64_t byte_off) {
 }
 
 // Ordered sum of lds[lo..hi) into acc, left to right: the LDS reads are
-// issued 4 at a time (one LDS latency per 4 nonzeros instead of per nonzero)
-// but the additions stay in sequence, so the rounding is omp_spmv's.
+// issued 4 at a time (one LDS latency per 4 nonzeros instead of per nonzero),
+// the last 1-3 together (C4's 10-nonzero rows: 54.2 -> 51.7 us,
+// profiles/r01_ab_ordered_sum_tail.jsonl), but the additions stay in
+// sequence, so the rounding is omp_spmv's.
+// (An 8-wide batch for the dictionary kernels measured flat on C3, -0.4 %.)
 template <typename T>
 __device__ __forceinline__ T ordered_sum(T acc, const T *lds, int32_t lo, int32_t hi) {
   int32_t k = lo;
@@ -134,7 +137,12 @@ __device__ __forceinline__ T ordered_sum(T acc, const T *lds, int32_t lo, int32_
     acc = acc + a2;
     acc = acc + a3;
   }
-  for (; k < hi; ++k) acc = acc + lds[k];
+  if (k < hi) {  // the last 1-3 in one LDS round trip (clamped reads, selected adds)
+    const T a0 = lds[k], a1 = lds[min(k + 1, hi - 1)], a2 = lds[min(k + 2, hi - 1)];
+    acc = acc + a0;
+    if (k + 1 < hi) acc = acc + a1;
+    if (k + 2 < hi) acc = acc + a2;
+  }
   return acc;
 }
 
