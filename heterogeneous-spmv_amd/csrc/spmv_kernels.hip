@@ -314,7 +314,10 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   // HSPMV_YNT / HSPMV_NT (0/1) override, for A/B runs.
   const bool hbm = footprint > 192.0 * 1024 * 1024;
   p.y_nt = hbm;
-  if (!p.nontemporal && hbm && A.col_span_bits > 17 && (double)A.n * sv > 4.0 * 1024 * 1024)
+  // (not on x-slab passes, whose gathers are L2-resident anyway: C5 284 ->
+  // 265 us with plain loads, profiles/r01_ab_nt_slabs.jsonl)
+  if (!p.nontemporal && hbm && A.col_span_bits > 17 && (double)A.n * sv > 4.0 * 1024 * 1024 &&
+      A.n_slabs <= 1)
     p.nontemporal = true;
   if (const char *e = getenv("HSPMV_YNT")) p.y_nt = atoi(e) != 0;
   if (const char *e = getenv("HSPMV_NT")) p.nontemporal = atoi(e) != 0;
