@@ -751,8 +751,10 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
     s.h_xwin.clear();
     s.h_xwin_t.clear();
     s.A.col_span_bits = 1;
+    s.A.has_xdict = s.xd_shape == kStream;
     return HSPMV_OK;
   }
+  s.A.has_xwin = !s.h_xwin.empty();
   bool c16 = false;
   if (kern == kStream && (rc = build_col16g(s, rp, col, m, n, dtype, flags, &c16))) return rc;
   if (!c16 && (rc = build_col16(s, col, rp[m], m, n, dtype, flags, &c16))) return rc;
@@ -865,7 +867,8 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     s.A.n_cplanes = 0;
   }
   if (s.xd_shape) {
-    const bool fits = (s.xd_shape == kStream && s.plan.kernel == kStream && s.plan.groups == 1) ||
+    const bool fits = (s.xd_shape == kStream && s.plan.kernel == kStream && s.plan.groups == 1 &&
+                       s.plan.waves_per_block == 4) ||
                       (s.xd_shape == kCsr3 && s.plan.kernel == kCsr3 && !s.h_tasks.empty() &&
                        s.plan.waves_per_block == s.A.task_waves);
     if (fits) {

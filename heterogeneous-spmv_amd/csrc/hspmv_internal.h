@@ -27,6 +27,9 @@ struct DevCSR {
   // nonzero's 64-row group, when every group's columns span < 65536
   int32_t c16_mode = 1;
   int32_t col_span_bits = 0;  // bits of the widest 256-nonzero block's column span (0 = unknown)
+  // planner hints from the host tables: STREAM x windows / block x
+  // dictionaries were built for this shard
+  bool has_xwin = false, has_xdict = false;
   int32_t n_slabs = 1;        // x slabs: the row kernel's passes (each sees ~nnz / n_slabs)
   int32_t task_waves = 4;     // CSR3 packed tasks per workgroup (4, or 8 with x dictionaries)
 };

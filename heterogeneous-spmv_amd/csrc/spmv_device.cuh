@@ -409,13 +409,14 @@ __device__ __forceinline__ void stage_xdict(T *xs, const T *__restrict__ x, cons
 // w * groups * 64, loading the next group's row pointers before streaming
 // the current one.  XW: groups whose x window (xwin[g] = {lo, w}) fits
 // kXWin entries gather from an LDS copy of it.
-template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD>
-__global__ __launch_bounds__(256) void hspmv_csr_stream(
+template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD, int W = 4>
+__global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
     int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups, int32_t y_nt, int32_t carry,
     const int32_t *__restrict__ rp, ColSrc cs, const int2 *__restrict__ xwin, XDict xd,
     const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
-  __shared__ T lds[4 * kWave * U];
-  __shared__ T xlds[XW ? 4 * kXWin : 1];
+  static_assert(!XD || W == 4, "dictionaries are planned for 256-row blocks");
+  __shared__ T lds[W * kWave * U];
+  __shared__ T xlds[XW ? W * kXWin : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char xdyn[];  // XD: the block's xs
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
@@ -423,13 +424,13 @@ __global__ __launch_bounds__(256) void hspmv_csr_stream(
   // XD (groups == 1): the block's 256 rows share one staged dictionary; the
   // only block barrier of the kernel is at the end of the staging.
   if constexpr (XD) stage_xdict<T, 256>(reinterpret_cast<T *>(xdyn), x, xd, blk, threadIdx.x);
-  int64_t g0 = (blk * 4 + wid) * (int64_t)groups * kWave;
+  int64_t g0 = (blk * W + wid) * (int64_t)groups * kWave;
   if (g0 >= m) return;  // wave-uniform
   const int64_t gend = min<int64_t>(g0 + (int64_t)groups * kWave, m);
   T *my = lds + wid * kWave * U;
   unsigned long long *ts = nullptr;
 #if (HSPMV_DIAG & 8)
-  const int64_t wv = blk * 4 + wid;
+  const int64_t wv = blk * W + wid;
   if (wv < kTraceWaves) ts = g_trace + wv * kTraceSlots;
   HSPMV_TRACE(ts, 0, diag_stamp());
   {
@@ -542,6 +543,26 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
     if constexpr (XD)
       hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, false, false, true>),
                          dim3((unsigned)p.blocks), dim3(256), dyn, st, A.m, dp.long_t,
+                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
+                         xw, xd, val, x, y);
+    else if (p.waves_per_block == 1 && xw)
+      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true, false, 1>),
+                         dim3((unsigned)p.blocks), dim3(64), dyn, st, A.m, dp.long_t,
+                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
+                         xw, xd, val, x, y);
+    else if (p.waves_per_block == 1)
+      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false, false, 1>),
+                         dim3((unsigned)p.blocks), dim3(64), dyn, st, A.m, dp.long_t,
+                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
+                         xw, xd, val, x, y);
+    else if (p.waves_per_block != 4 && xw)
+      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true, false, 2>),
+                         dim3((unsigned)p.blocks), dim3(128), dyn, st, A.m, dp.long_t,
+                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
+                         xw, xd, val, x, y);
+    else if (p.waves_per_block != 4)
+      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false, false, 2>),
+                         dim3((unsigned)p.blocks), dim3(128), dyn, st, A.m, dp.long_t,
                          (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
                          xw, xd, val, x, y);
     else if (xw)

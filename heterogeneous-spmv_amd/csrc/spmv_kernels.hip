@@ -275,7 +275,20 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
       const unsigned gcode = (flags >> 29) & 0x7u;  // HSPMV_GROUPS(g)
       p.groups = gcode ? 1 << (gcode - 1) : 1;
       const int64_t waves = (tasks + p.groups - 1) / p.groups;
-      p.blocks = (waves + 3) / 4;
+      // waves per workgroup.  The STREAM waves never meet at a barrier, so
+      // small workgroups free their CU slots wave by wave: one wave per
+      // workgroup for Infinity-Cache-resident matrices and LDS-windowed
+      // gathers (C2 bench 737 -> 760 GFLOP/s, C4 53.2 -> 50.4 us), two for
+      // HBM gathers, where one-wave workgroups run into the per-CU workgroup
+      // limit (honeycomb 166.0 -> 161.8 us with two, flat with one; l4k
+      // 211.2 -> 207.5).  Four (the dictionaries' 256-row blocks) with x
+      // dictionaries; profiles/r01_ab_stream_w.jsonl.
+      p.waves_per_block = A.has_xdict ? 4 : ((footprint <= 192.0 * 1024 * 1024 || A.has_xwin) ? 1 : 2);
+      if (const char *e = getenv("HSPMV_STREAM_W")) {
+        const int w = atoi(e);
+        if ((w == 1 || w == 2 || w == 4) && !A.has_xdict) p.waves_per_block = w;
+      }
+      p.blocks = (waves + p.waves_per_block - 1) / p.waves_per_block;
       break;
     }
     case kCsr3: {

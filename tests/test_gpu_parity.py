@@ -617,3 +617,36 @@ def test_full_size_fp32_bitwise_vs_reference_omp_spmv(cfg):
     absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x.astype(np.float64))
     err = np.abs(y.astype(np.float64) - y_ref.astype(np.float64))
     assert np.all(err <= (np.diff(A.row_ptr) + 2) * 2.0 ** -23 * absrow + 1e-30)
+
+
+def test_stream_workgroup_sizes_identical(monkeypatch):
+    """STREAM with 1, 2 and 4 waves per workgroup (HSPMV_STREAM_W; the
+    planner picks 1 for cache-resident / x-windowed matrices, 2 otherwise,
+    4 with x dictionaries): bit-identical y, including x windows, several
+    groups per wave, split rows and a row count that is not a multiple of
+    64."""
+    rng = np.random.default_rng(4)
+    lens = rng.integers(0, 40, 3001)
+    lens[:70] = 0
+    lens[-90:] = 0
+    rp = np.concatenate([[0], np.cumsum(lens)])
+    ragged = hspmv.CsrMatrix(3001, 5000, rp, np.concatenate(
+        [np.sort(rng.choice(5000, n, replace=False)) for n in lens]).astype(np.int32),
+        rng.uniform(-1, 1, rp[-1]))
+    cases = [gen.laplace2d(300, 200), gen.banded(30000, per_row=10, half=32, seed=5),
+             _split_row_matrix(), ragged]
+    for A in cases:
+        x = gen.rand_x(A.n, 3)
+        for kw in (dict(kernel="stream"), dict(kernel="stream", groups_per_wave=2),
+                   dict(kernel="stream", col16=True)):
+            ys = []
+            for w in ("1", "2", "4"):
+                monkeypatch.setenv("HSPMV_STREAM_W", w)
+                y, info = gpu_spmv(A, x, **kw)
+                assert info["waves_per_block"] == int(w), (kw, w, info["waves_per_block"])
+                ys.append(y)
+            assert all(np.array_equal(ys[0].view(np.uint8), v.view(np.uint8)) for v in ys[1:]), kw
+        check_fp64(A, x, ys[0], exact_rows=short_rows(A))
+    monkeypatch.delenv("HSPMV_STREAM_W")
+    _, info = gpu_spmv(gen.laplace2d(300, 200), gen.rand_x(60000, 1))
+    assert info["waves_per_block"] == 1  # cache-resident: one wave per workgroup
