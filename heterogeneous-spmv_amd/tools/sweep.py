@@ -51,6 +51,10 @@ def build(cfg):
         A = gen.stencil27(125)
         maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
         return A, maps, "C3 27-pt 125^3 RCM CSR-3 fp64 (mi355x grouping ssrs=64, srs=4)"
+    if cfg.startswith("c2s"):  # C2's matrix, CSR-3 grouping (ssrs, srs) = c2s<ssrs>x<srs>
+        ssrs, srs = (int(v) for v in cfg[3:].split("x"))
+        A = gen.laplace2d(1000, 1000)
+        return A, hspmv.build_csr3_maps(A, ssrs, srs), f"C2 CSR-3 fp64 (ssrs={ssrs}, srs={srs})"
     if cfg.startswith("c3s"):  # C3's matrix, CSR-3 grouping (ssrs, srs) = c3s<ssrs>x<srs>
         ssrs, srs = (int(v) for v in cfg[3:].split("x"))
         A = gen.stencil27(125)
