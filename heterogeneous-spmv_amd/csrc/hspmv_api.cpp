@@ -66,6 +66,7 @@ struct Shard {
   int32_t *d_slab_col = nullptr;     // slab-major columns and values
   void *d_slab_val = nullptr;
   int32_t n_slabs = 0;
+  int c16g_shape = 0;                // group-base columns built for kStream groups / kCsr3 tasks
   std::vector<int32_t> h_xwin;       // built at upload (host columns at hand)
   std::vector<int32_t> h_xwin_t;     // the same per packed CSR-3 task
   void *d_val = nullptr;
@@ -256,8 +257,10 @@ int build_col16(Shard &s, const int32_t *col, int64_t nnz, int64_t m, int64_t n,
 // us with group bases, c3h/l4k within 1 %; profiles/r01_ab_col16_group*.jsonl).
 // HSPMV_COL16G=0 disables, =1 uses it whenever it fits.  Split rows (read
 // by the split-row kernels from the 32-bit columns) get offset 0.
+// Row groups: STREAM's 64-row groups (starts == nullptr) or the packed CSR3
+// wave tasks [starts[g], starts[g+1]).
 int build_col16g(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int64_t n, int dtype,
-                 unsigned flags, bool *used) {
+                 unsigned flags, const std::vector<int32_t> *starts, bool *used) {
   *used = false;
   const char *env = getenv("HSPMV_COL16G");
   const int mode = env ? atoi(env) : -1;  // -1 auto, 0 off, 1 on whenever it fits
@@ -268,7 +271,12 @@ int build_col16g(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int
   if (!forced && (double)nnz * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv > kMallResident)
     return HSPMV_OK;
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
-  const int64_t ng = (m + 63) / 64;
+  const int64_t ng = starts ? (int64_t)starts->size() - 1 : (m + 63) / 64;
+  if (ng <= 0) return HSPMV_OK;
+  auto rows = [&](int64_t g, int64_t &r0, int64_t &r1) {
+    r0 = starts ? (*starts)[(size_t)g] : 64 * g;
+    r1 = starts ? (*starts)[(size_t)g + 1] : std::min(m, 64 * g + 64);
+  };
   std::vector<int32_t> base((size_t)ng + 1, 0);  // +1: read by 8-byte scalar loads
   std::vector<int32_t> span((size_t)ng, 0);
   const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, ng / 4096));
@@ -280,7 +288,9 @@ int build_col16g(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int
   par([&](int64_t g0, int64_t g1) {
     for (int64_t g = g0; g < g1; ++g) {
       int32_t lo = INT32_MAX, hi = -1;
-      for (int64_t r = 64 * g; r < std::min(m, 64 * g + 64); ++r) {
+      int64_t ra, rb;
+      rows(g, ra, rb);
+      for (int64_t r = ra; r < rb; ++r) {
         if (rp[r + 1] - rp[r] > long_t) continue;
         for (int32_t k = rp[r]; k < rp[r + 1]; ++k) {
           lo = std::min(lo, col[k]);
@@ -296,11 +306,14 @@ int build_col16g(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int
   if (maxspan > 65535) return HSPMV_OK;
   std::vector<uint16_t> off((size_t)nnz, 0);
   par([&](int64_t g0, int64_t g1) {
-    for (int64_t g = g0; g < g1; ++g)
-      for (int64_t r = 64 * g; r < std::min(m, 64 * g + 64); ++r) {
+    for (int64_t g = g0; g < g1; ++g) {
+      int64_t ra, rb;
+      rows(g, ra, rb);
+      for (int64_t r = ra; r < rb; ++r) {
         if (rp[r + 1] - rp[r] > long_t) continue;
         for (int32_t k = rp[r]; k < rp[r + 1]; ++k) off[(size_t)k] = (uint16_t)(col[k] - base[(size_t)g]);
       }
+    }
   });
   int rc;
   if ((rc = dev_alloc(&s.d_c16, 2 * (size_t)nnz, &s.bytes))) return rc;
@@ -315,6 +328,7 @@ int build_col16g(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int
   s.A.cplanes = nullptr;
   s.A.n_cplanes = 0;
   s.A.c16_mode = 2;
+  s.c16g_shape = starts ? kCsr3 : kStream;
   *used = true;
   return HSPMV_OK;
 }
@@ -756,7 +770,8 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
   }
   s.A.has_xwin = !s.h_xwin.empty();
   bool c16 = false;
-  if (kern == kStream && (rc = build_col16g(s, rp, col, m, n, dtype, flags, &c16))) return rc;
+  if (kern == kStream && (rc = build_col16g(s, rp, col, m, n, dtype, flags, nullptr, &c16))) return rc;
+  if (kern == kCsr3 && (rc = build_col16g(s, rp, col, m, n, dtype, flags, &s.h_tasks, &c16))) return rc;
   if (!c16 && (rc = build_col16(s, col, rp[m], m, n, dtype, flags, &c16))) return rc;
   return HSPMV_OK;
 }
@@ -883,11 +898,13 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     } else {  // planned for another block shape: the kernels read the 32-bit columns
       s.A.col16 = nullptr;
     }
-  } else if (s.A.col16 && s.A.c16_mode == 2 && s.plan.kernel != kStream) {
-    s.A.col16 = nullptr;  // group bases were built for STREAM's groups: 32-bit columns
+  } else if (s.A.col16 && s.A.c16_mode == 2 &&
+             (s.plan.kernel != s.c16g_shape || (s.plan.kernel == kCsr3 && s.h_tasks.empty()))) {
+    s.A.col16 = nullptr;  // group bases built for another row grouping: 32-bit columns
     s.A.cbase = nullptr;
   } else if (s.A.col16 && s.A.c16_mode == 2) {
-    s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)((s.A.m + 63) / 64);
+    const int64_t ngb = s.plan.kernel == kCsr3 ? (int64_t)s.h_tasks.size() - 1 : (s.A.m + 63) / 64;
+    s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)ngb;
   } else if (s.A.col16) {
     const int64_t nb = (s.A.nnz + (int64_t(1) << kC16Shift) - 1) >> kC16Shift;
     s.c16_saved = 2.0 * (double)(s.A.nnz - long_nnz) - 4.0 * (double)nb -

@@ -493,6 +493,9 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
   const int32_t r1 = (int32_t)(tb >> 32);
   if (r0 >= r1) return;
   T *my = lds + wid * kWave * U;
+  // group-base columns: one base per packed task
+  int32_t gbase = 0;
+  if constexpr (C16 == 2) gbase = (int32_t)sload_i64(cs.cbase, (uint64_t)t * 4u);
   XWin<T> win{XD ? reinterpret_cast<const T *>(xdyn) : nullptr, 0, 0};
   if constexpr (XW) {  // the task's x window (packed tasks: <= 64 rows)
     const int64_t wv = sload_i64(xwin, (uint64_t)t * 8u);
@@ -517,7 +520,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
     wave_rows<T, NT, U, PF, C16, XW, XD>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                         win, y_nt != 0, carry != 0, 0, ts);
+                                         win, y_nt != 0, carry != 0, gbase, ts);
     ts = nullptr;
     beg = nbeg;
     end = nend;
@@ -577,9 +580,7 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
                          xw, xd, val, x, y);
     return;
   }
-  if constexpr (C16 == 2) {
-    return;  // group-base offsets are built for STREAM's groups only (launch_rows checks)
-  } else {
+  {
   const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
 #define HSPMV_CSR3(W, C, XW, X)                                                               \
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C, W, XW, X>), dim3((unsigned)p.blocks),      \
@@ -644,7 +645,8 @@ hipError_t launch_rows(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, 
     return launch_rows_c<T, 0, true>(A, dp, p, x, y, st);
   }
   if (A.col16 && A.c16_mode == 2) {
-    if (p.kernel != kStream) return hipErrorInvalidValue;  // built for STREAM's groups
+    if (p.kernel == kCsr3 && (!dp.task_start || p.waves_per_block != 4))
+      return hipErrorInvalidValue;  // built for the packed tasks, 4 per workgroup
     return launch_rows_c<T, 2, false>(A, dp, p, x, y, st);
   }
   return A.col16 ? launch_rows_c<T, 1, false>(A, dp, p, x, y, st)

@@ -418,7 +418,8 @@ def test_col16_offsets_bitwise_and_fallback(monkeypatch):
     per-256-nonzero block bases + p high-bit planes (forced here with
     HSPMV_COL16G=0, p <= 8; p grows with a block's column span and a matrix
     needing more than 8 planes keeps 32-bit columns), and one base per
-    64-row STREAM group (HSPMV_COL16G=1) when every group spans < 65536.
+    64-row STREAM group or packed CSR3 task (HSPMV_COL16G=1) when every
+    group spans < 65536.
     By default these small (Infinity-Cache-resident) matrices use the group
     bases where they fit and 32-bit columns otherwise."""
     cases = [(gen.laplace2d(300, 200), 1, True),                  # spans < 65536
@@ -444,7 +445,7 @@ def test_col16_offsets_bitwise_and_fallback(monkeypatch):
                 assert i16["col16"] == want, (kw, i16["col16"], want)
             if i16["col16"]:
                 assert i16["format_bytes"] < i16["alg_bytes"]
-            g = group_fits and kw["kernel"] == "stream"
+            g = group_fits  # STREAM's 64-row groups or CSR3's packed tasks
             assert i16g["col16_group"] == int(g), (kw, i16g["col16_group"])
             if g:
                 assert i16g["col16"] == 1 and i16g["format_bytes"] < i16g["alg_bytes"]
