@@ -134,8 +134,9 @@ typedef struct {
                          row kernel runs over, one pass each, so irregular
                          gathers stay in an L2-sized slice of x (GPU 0)     */
   int32_t col16_group; /* 1 = the 16-bit column offsets are relative to one
-                          base per 64-row STREAM group (every group's columns
-                          span < 65536); 0 = per 256-nonzero blocks or none  */
+                          base per 64-row STREAM group or packed CSR3 task
+                          (every one spans < 65536 columns); 0 = per
+                          256-nonzero blocks or none                        */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
