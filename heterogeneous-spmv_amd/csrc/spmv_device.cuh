@@ -615,6 +615,7 @@ hipError_t launch_rows_pf(const DevCSR &A, const DevPlan &dp, const LaunchPlan &
     case 2: launch_rows_u<T, NT, 2, PF, C16, XD>(A, dp, p, x, y, st); break;
     case 3: launch_rows_u<T, NT, 3, PF, C16, XD>(A, dp, p, x, y, st); break;
     case 4: launch_rows_u<T, NT, 4, PF, C16, XD>(A, dp, p, x, y, st); break;
+    case 5: launch_rows_u<T, NT, 5, PF, C16, XD>(A, dp, p, x, y, st); break;
     case 6: launch_rows_u<T, NT, 6, PF, C16, XD>(A, dp, p, x, y, st); break;
     case 8: launch_rows_u<T, NT, 8, PF, C16, XD>(A, dp, p, x, y, st); break;
     case 16: launch_rows_u<T, NT, 16, PF, C16, XD>(A, dp, p, x, y, st); break;

@@ -212,6 +212,9 @@ int pick_u(double nnz_per_pass, int dtype, bool slabs) {
   if (nnz_per_pass <= 128.0) return 2;
   if (nnz_per_pass <= 192.0) return 3;
   if (nnz_per_pass <= 256.0) return 4;
+  // 5-nonzero rows fill U = 5 exactly (C2 14.76 -> 14.28 us, l4k 208 -> 199;
+  // profiles/r01_ab_u5.jsonl)
+  if (nnz_per_pass <= 320.0) return 5;
   if (nnz_per_pass <= 384.0) return 6;
   if (nnz_per_pass <= 768.0) return 6;  // two chunks (C4 fp64: -1.5 %, r01_ab_col16)
   if (dtype == 1) return 4;

@@ -291,8 +291,8 @@ class SpMV:
         flags |= _lib.col16_flag(col16)
         flags |= (0 if split_rows else _lib.FLAG_NO_SPLIT)
         if chunk_u:
-            if chunk_u not in (2, 3, 4, 6, 8, 16):
-                raise ValueError("chunk_u must be one of 2, 3, 4, 6, 8, 16")
+            if chunk_u not in (2, 3, 4, 5, 6, 8, 16):
+                raise ValueError("chunk_u must be one of 2, 3, 4, 5, 6, 8, 16")
             flags |= chunk_u << _lib.U_SHIFT
         if prefetch:
             flags |= _lib.FLAG_PREFETCH

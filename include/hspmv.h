@@ -165,7 +165,7 @@ typedef struct hspmv_handle hspmv_handle;
  * HBM-resident matrices stream faster in dispatch order (profiles/r01_sweep*). */
 #define HSPMV_FLAG_NO_SPLIT (1u << 15)     /* no split-row kernels: very
                                               long rows stay on one wave   */
-/* STREAM/CSR3 elements per lane per LDS chunk: HSPMV_U(u), u in {2,3,4,6,8,16};
+/* STREAM/CSR3 elements per lane per LDS chunk: HSPMV_U(u), u in {2,3,4,5,6,8,16};
  * 0 = auto from the mean row length */
 #define HSPMV_U_SHIFT 16
 #define HSPMV_U(u) ((unsigned)(u) << HSPMV_U_SHIFT)

@@ -328,7 +328,7 @@ def test_chunk_u_and_remap_variants():
         x = gen.rand_x(A.n, 6)
         ys = []
         maps = hspmv.build_csr3_maps(A, 20, 10)
-        for u in (2, 3, 4, 6, 8, 16):
+        for u in (2, 3, 4, 5, 6, 8, 16):
             for remap, pf in ((True, False), (False, True), (True, True)):
                 y, info = gpu_spmv(A, x, kernel="stream", chunk_u=u, xcd_remap=remap, prefetch=pf)
                 assert info["chunk_u"] == u and (info["xcd_remap"] > 1) == remap
