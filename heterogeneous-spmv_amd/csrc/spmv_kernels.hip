@@ -216,7 +216,12 @@ int pick_u(double nnz_per_pass, int dtype, bool slabs) {
   // profiles/r01_ab_u5.jsonl)
   if (nnz_per_pass <= 320.0) return 5;
   if (nnz_per_pass <= 384.0) return 6;
-  if (nnz_per_pass <= 768.0) return 6;  // two chunks (C4 fp64: -1.5 %, r01_ab_col16)
+  // two chunks, as full as possible: C4's 640-nonzero groups take 2 x 320
+  // (U = 5: fp64 51.1 -> 50.2 us, fp32 35.0 -> 33.0; r01_ab_u5.jsonl)
+  if (nnz_per_pass <= 768.0) {
+    const int u = (int)((nnz_per_pass + 127.0) / 128.0);
+    return u <= 4 ? 4 : (u == 5 ? 5 : 6);
+  }
   if (dtype == 1) return 4;
   return slabs ? 8 : 16;
 }
