@@ -126,7 +126,8 @@ __device__ __forceinline__ int64_t sload_i64(const void *p, uint64_t byte_off) {
 // the last 1-3 together (C4's 10-nonzero rows: 54.2 -> 51.7 us,
 // profiles/r01_ab_ordered_sum_tail.jsonl), but the additions stay in
 // sequence, so the rounding is omp_spmv's.
-// (An 8-wide batch for the dictionary kernels measured flat on C3, -0.4 %.)
+// (An 8-wide batch for the dictionary kernels measured flat on C3, -0.4 %;
+// 8-wide clamped batches everywhere slower: C3 +13 %, honeycomb +5 %.)
 template <typename T>
 __device__ __forceinline__ T ordered_sum(T acc, const T *lds, int32_t lo, int32_t hi) {
   int32_t k = lo;
