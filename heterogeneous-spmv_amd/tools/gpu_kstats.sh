@@ -1,0 +1,20 @@
+# GPU-box pass: rocprofv3 --kernel-trace --stats over tools/run_one.py for each
+# non-bench config (C3 CSR-3, hugebubbles stand-in, C4 shard, C5, C3 fp32),
+# summaries under gpurun_out/<TAG>_kstats/.
+# Usage (from the repo root): bash heterogeneous-spmv_amd/tools/gpu_kstats.sh [TAG]
+set -o pipefail
+TAG=${1:-r01}
+R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out/${TAG}_kstats
+export PYTHONUNBUFFERED=1
+O=$R/gpurun_out/${TAG}_kstats
+cd /tmp && export TMPDIR=/tmp
+for cfg in c3 c3h c4 c5 c3:f32; do
+  name=${cfg/:/_}
+  echo "== $cfg"
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$name -o run \
+    -- python3 $R/heterogeneous-spmv_amd/tools/run_one.py --config $cfg --iters 100 \
+    > $O/${name}_run.log 2>&1 || exit $?
+  tail -1 $O/${name}_run.log > $O/${name}_run.json
+  cp $O/prof_$name/*kernel_stats.csv $O/${name}_kernel_stats.csv
+  head -c 300 $O/${name}_run.json; echo
+done
