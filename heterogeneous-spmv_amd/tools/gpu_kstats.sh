@@ -14,7 +14,7 @@ for cfg in c3 c3h c4 c5 c3:f32; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$name -o run \
     -- python3 $R/heterogeneous-spmv_amd/tools/run_one.py --config $cfg --iters 100 \
     > $O/${name}_run.log 2>&1 || exit $?
-  tail -1 $O/${name}_run.log > $O/${name}_run.json
+  grep '^{' $O/${name}_run.log > $O/${name}_run.json
   cp $O/prof_$name/*kernel_stats.csv $O/${name}_kernel_stats.csv
   head -c 300 $O/${name}_run.json; echo
 done
