@@ -8,29 +8,39 @@ HBM; no data-path collective -- rows are independent).
 W untimed steps, then exactly K steps bracketed by barrier + synchronize; the
 max over ranks is the step time; rank 0 prints ONE JSON line.
 
-Workload (default ``--config c2``): BASELINE configs[1], CSR fp64 on the 2-D
-5-point Laplacian 1000 x 1000 (m = 1e6, nnz = 4,996,000) per GPU; at N GPUs
-the global grid is 1000 x 1000N, row-range partitioned (weak scaling).
-``--config c4``: the 2e7-row banded matrix split over N GPUs (strong).
+Workload (``--config``, default by world size; hspmv.dist.default_config):
+  N = 1  c3: BASELINE configs[2], the largest single-GPU configuration --
+         CSR-3 fp64 on the 27-point 125^3 stencil, RCM-permuted
+         (m = 1,953,125, nnz = 51,895,117), maps (ssrs, srs) = (20, 10) from
+         the .csr3 writer heuristic; the hspmv_csr3 kernel.
+  N > 1  c4: BASELINE configs[3], the 2e7-row banded matrix (~200 M nnz)
+         row-range partitioned over the N GPUs, nnz-balanced (strong scaling).
+  Also: c2 (configs[1], weak scaling: 1000 x 1000 rows per GPU), c3h (the
+  hugebubbles-00000 stand-in), c5 (configs[4], CSR-3 fp32 power-law).
+``--dry-run`` prints the partition plan without touching a GPU.
 
 Extra fields on the line:
-  roofline     dominant kernel, algorithmic bytes per launch / event-timed
-               average launch duration on the launch stream, vs 8 TB/s HBM
-  cold         the same SpMV with the 256 MiB Infinity Cache flushed before
-               every launch (the C2 matrix, 80 MB, is MALL-resident when warm)
+  roofline     one SpMV (the kernel launch(es) of a step), algorithmic bytes
+               per SpMV / HIP-event-timed average over the timed region on
+               the launch stream, vs 8 TB/s HBM; traffic from the committed
+               rocprofv3 PMC summary for this workload (profiles/*_pmc.json)
+  cold         the same SpMV with the 256 MiB Infinity Cache evicted before
+               every launch (a 512 MiB read)
   comm         RCCL x broadcast / y all-gather / halo-exchange times (N > 1),
-               timed separately, and the end-to-end rates they imply:
-               2 nnz / (step + y all-gather), and the iterative form
-               2 nnz / (step + halo exchange) where x is distributed like y
+               timed separately, and the end-to-end rates they imply
   cpu_baseline the oracle's OpenMP restatement of spmv-csr's omp_spmv on the
-               host cores, rank 0 at N = 1 only (bounded sample); beside it,
-               reference_f32: the reference's own spmv-csr program (fp32)
+               host cores, on the SAME matrix (rank 0 at N = 1 only, bounded
+               sample), value from TimeMin as run_norm.py records it; beside
+               it reference_f32: the reference's own omp_spmv (spmv-csr/spmv.c,
+               built unmodified into oracle/_ref) on the fp32 copy
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -41,12 +51,6 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "heterogeneous-spmv_amd"))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402  (device memory, streams, torch.distributed: plumbing)
-import torch.distributed as dist  # noqa: E402
-
-import hspmv  # noqa: E402
-from hspmv import dist as hdist  # noqa: E402
-from hspmv import gen  # noqa: E402
 
 METRIC = "SpMV GFLOP/s and achieved HBM GB/s (fp64) per matrix, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
@@ -57,18 +61,50 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=["c2", "c4"])
-    ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "vector"])
+    ap.add_argument("--config", default="auto", choices=["auto", "c2", "c3", "c3h", "c4", "c5"],
+                    help="auto: c3 at N = 1, c4 at N > 1")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "vector", "csr3"])
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--nt", action="store_true", help="non-temporal matrix loads")
     ap.add_argument("--cold-steps", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print the workload and partition plan, touch no GPU")
+    a = ap.parse_args()
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if a.steps < 1 or a.warmup < 0:
+        ap.error("--steps must be >= 1 and --warmup >= 0")
+    return a
 
+
+def resolve_config(args) -> str:
+    from hspmv import dist as hdist
+    return hdist.default_config(args.gpus) if args.config == "auto" else args.config
+
+
+def dry_run(args) -> None:
+    """CPU-side plan: the configuration and the nnz-balanced row partition the
+    run would use (closed-form row lengths; no matrix is built)."""
+    from hspmv import dist as hdist
+    cfg = resolve_config(args)
+    out = {"dry_run": True, "n_gpus": args.gpus, "steps": args.steps, "warmup": args.warmup,
+           "config": cfg, "metric": METRIC}
+    try:
+        out["plan"] = hdist.plan_splits(cfg, args.gpus)
+    except ValueError:
+        out["plan"] = {"config": cfg, "world": args.gpus, "scaling": "strong",
+                       "note": "row lengths known only after generating the matrix"}
+    print(json.dumps(out), flush=True)
+
+
+# ------------------------------------------------------------------ torch plumbing
 
 def dist_setup(args):
+    import torch
+    import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -84,31 +120,28 @@ def dist_setup(args):
 
 
 def barrier(world):
+    import torch
+    import torch.distributed as dist
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
 
 
-def max_over_ranks(v: float, world: int) -> float:
+def reduce_over_ranks(v: float, world: int, op: str) -> float:
     if world == 1:
         return v
+    import torch
+    import torch.distributed as dist
     t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def sum_over_ranks(v: float, world: int) -> float:
-    if world == 1:
-        return v
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return float(t.item())
 
 
 def load_traffic(workload_key: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary
     (profiles/*_pmc.json, written by heterogeneous-spmv_amd/tools/pmc_summary.py),
-    or None when no summary for this workload exists."""
+    or None when no summary for this workload exists.  The newest file wins
+    (profiles are named per round, r01_ < r02_ ...)."""
     best = None
     for p in sorted((REPO / "profiles").glob("*_pmc.json")):
         try:
@@ -117,115 +150,170 @@ def load_traffic(workload_key: str):
             continue
         if d.get("workload") == workload_key and d.get("hbm_bytes_per_launch"):
             best = d
+            best["file"] = str(p.relative_to(REPO))
     return best
 
 
+# ------------------------------------------------------------------ CPU baseline
+
+def host_cpu_info() -> dict:
+    """Physical cores from lscpu (Core(s) per socket x Socket(s)), the CPUs
+    this process may run on, and the cgroup CPU quota (cpu.max), if any."""
+    info = {"physical_cores": None, "affinity_cpus": len(os.sched_getaffinity(0)),
+            "cgroup_cpu_quota": None, "model": None}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        kv = {}
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            kv[k.strip()] = v.strip()
+        cps, sock = int(kv.get("Core(s) per socket", "0")), int(kv.get("Socket(s)", "0"))
+        if cps and sock:
+            info["physical_cores"] = cps * sock
+        info["model"] = kv.get("Model name")
+    except Exception:
+        pass
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            info["cgroup_cpu_quota"] = float(q) / float(per)
+    except Exception:
+        pass
+    return info
+
+
 def cpu_baseline(A, x, budget_s: float):
-    """Oracle OpenMP restatement of omp_spmv (spmv-csr/spmv.c:92-114) timed with
-    the reference protocol (5 warm-ups + timed runs), on this host's cores."""
+    """The oracle's OpenMP restatement of omp_spmv (spmv-csr/spmv.c:92-114) on
+    the same matrix, timed with the reference protocol (5 warm-ups + N timed
+    runs, omp_get_wtime per run; spmv.c:164-185) on this host's cores.  The
+    thread count tried first is the physical core count (lscpu), capped by
+    the CPUs this process may use and the cgroup quota; OMP_NUM_THREADS (the
+    box's CPU share) is tried beside it, and the faster TimeMin is reported.
+    value = 2 nnz / TimeMin (run_norm.py records min/max/avg)."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = min(threads, os.cpu_count() or threads)
+    hw = host_cpu_info()
+    phys = hw["physical_cores"] or hw["affinity_cpus"]
+    cand = {max(1, min(phys, hw["affinity_cpus"]))}
+    if hw["cgroup_cpu_quota"]:
+        cand.add(max(1, min(phys, hw["affinity_cpus"], int(math.ceil(hw["cgroup_cpu_quota"])))))
+    env_t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env_t > 0:
+        cand.add(min(env_t, hw["affinity_cpus"]))
+    tried = {}
+    for t in sorted(cand):
+        oracle.set_schedule("static", t)
+        tmin, tmax, tavg, used = oracle.time_spmv(A.row_ptr, A.col_idx, A.val, x, warmup=5, runs=20)
+        tried[int(used)] = {"time_min_s": tmin, "time_avg_s": tavg,
+                            "gflops_from_min": round(2.0 * A.nnz / tmin * 1e-9, 3)}
+    threads = min(tried, key=lambda t: tried[t]["time_min_s"])
+    per = max(tried[threads]["time_avg_s"], 1e-6)
+    runs = int(max(20, min(20000, 0.5 * budget_s / per)))
     res = {}
     for sched in ("static", "guided"):  # run_norm.py:18,66 / run_cuda_new.py:79
         oracle.set_schedule(sched, threads)
-        tmin, tmax, tavg, used = oracle.time_spmv(A.row_ptr, A.col_idx, A.val, x, warmup=5, runs=20)
-        runs = int(max(20, min(20000, budget_s / max(tavg, 1e-6))))
-        tmin, tmax, tavg, used = oracle.time_spmv(A.row_ptr, A.col_idx, A.val, x, warmup=5,
-                                                  runs=runs)
-        res[sched] = (tmin, tmax, tavg, int(used), runs)
-    tmin, tmax, tavg, used, runs = res["static"]
+        res[sched] = oracle.time_spmv(A.row_ptr, A.col_idx, A.val, x, warmup=5, runs=runs)
+    tmin, tmax, tavg, used = res["static"]
     g = res["guided"]
-    return {"value": round(2.0 * A.nnz / tavg * 1e-9, 3), "unit": "GFLOP/s", "cores": used,
+    dt = "fp64" if A.val.dtype == np.float64 else "fp32"
+    return {"value": round(2.0 * A.nnz / tmin * 1e-9, 3), "unit": "GFLOP/s", "cores": int(used),
             "kind": "port",
-            "sample": (f"full C2 matrix (m={A.m}, nnz={A.nnz}) fp64, omp_spmv restatement "
-                       f"(oracle/spmv_oracle.c), OMP_SCHEDULE=static, 5 warm-ups + {runs} timed "
-                       f"runs (spmv-csr/spmv.c:164-185 protocol), value from TimeAvg"),
+            "sample": (f"the same matrix as the GPU line (m={A.m}, nnz={A.nnz}, {dt}, CSR), "
+                       f"omp_spmv restatement (oracle/spmv_oracle.c), OMP_SCHEDULE=static, "
+                       f"{int(used)} threads, 5 warm-ups + {runs} timed runs "
+                       f"(spmv-csr/spmv.c:164-185 protocol), value = 2 nnz / TimeMin"),
             "time_min_s": tmin, "time_avg_s": tavg, "time_max_s": tmax,
-            "gflops_from_min": round(2.0 * A.nnz / tmin * 1e-9, 3),
-            "guided": {"gflops": round(2.0 * A.nnz / g[2] * 1e-9, 3),
-                       "gflops_from_min": round(2.0 * A.nnz / g[0] * 1e-9, 3),
-                       "time_avg_s": g[2], "runs": g[4]}}
+            "gflops_from_avg": round(2.0 * A.nnz / tavg * 1e-9, 3),
+            "host": hw, "threads_tried": tried,
+            "guided": {"gflops": round(2.0 * A.nnz / g[0] * 1e-9, 3),
+                       "gflops_from_avg": round(2.0 * A.nnz / g[2] * 1e-9, 3),
+                       "time_min_s": g[0], "time_avg_s": g[2], "runs": runs}}, threads
 
 
-def reference_cpu(A, runs: int = 200):
-    """The reference's own spmv-csr program (spmv-csr/spmv.c main, built
+def reference_cpu(A, x, threads: int, budget_s: float):
+    """The reference's own omp_spmv (spmv-csr/spmv.c:92-114, compiled
     unmodified from /root/reference into oracle/_ref by oracle/Makefile) on
-    the fp32 version of the workload, run in a child process exactly as
-    `spmv.exe file.csr runs`: its reader, x = 1, `runs` serial test_spmv
-    calls, 5 warm-ups and `runs` timed omp_spmv calls (OMP_SCHEDULE=static,
-    run_norm.py:18).  Returns its TimeMin/TimeAvg, or None when the library
-    was not built (no /root/reference where build() ran)."""
-    import subprocess
-    import tempfile
-    lib = REPO / "oracle" / "_ref" / "libref_spmvcsr.so"
-    if not lib.exists():
+    the fp32 copy of the same matrix (its only dtype), same protocol: 5
+    warm-ups + N timed calls.  None when the library was not built."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import ctypes as C
+    import oracle
+    if not oracle.ref_available():
         return None
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    with tempfile.TemporaryDirectory() as d:
-        path = os.path.join(d, "c2.mtx.rcm.csr")
-        hspmv.write_csr(path, A.astype(np.float32))  # the reference's text format (A15)
-        code = ("import ctypes, sys; L = ctypes.CDLL(sys.argv[1]); "
-                "a = (ctypes.c_char_p * 3)(b'spmv.exe', sys.argv[2].encode(), sys.argv[3].encode()); "
-                "L.ref_main(3, a)")
-        env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_SCHEDULE="static")
-        try:
-            out = subprocess.run([sys.executable, "-c", code, str(lib), path, str(runs)], env=env,
-                                 capture_output=True, text=True, timeout=180)
-        except subprocess.TimeoutExpired:
-            return None
-    vals = {}
-    for line in out.stdout.splitlines():  # parsed like run_norm.py:94-107
-        for key in ("TimeMin:", "TimeMax:", "TimeAvg:"):
-            if line.startswith(key):
-                vals[key[:-1]] = float(line[len(key):].strip())
-    if out.returncode != 0 or "TimeAvg" not in vals:
-        return None
+    R = oracle.ref()
+    oracle.set_schedule("static", threads)
+    rp = np.ascontiguousarray(A.row_ptr, np.int32)
+    ci = np.ascontiguousarray(A.col_idx, np.int32)
+    v = np.ascontiguousarray(A.val, np.float32)
+    xx = np.ascontiguousarray(x, np.float32)
+    y = np.zeros(A.m, np.float32)
+    args = (C.c_int(A.m), C.c_int(xx.shape[0]), C.c_int(A.nnz), rp.ctypes.data, ci.ctypes.data,
+            v.ctypes.data, xx.ctypes.data, y.ctypes.data)
+    for _ in range(5):
+        R.omp_spmv(*args)
+    ts = []
+    t_end = time.perf_counter() + budget_s
+    while len(ts) < 20 or (time.perf_counter() < t_end and len(ts) < 20000):
+        t0 = time.perf_counter()
+        R.omp_spmv(*args)
+        ts.append(time.perf_counter() - t0)
+    tmin, tavg = min(ts), sum(ts) / len(ts)
     return {"kind": "reference", "dtype": "f32", "cores": threads,
-            "value": round(2.0 * A.nnz / vals["TimeAvg"] * 1e-9, 3), "unit": "GFLOP/s",
-            "gflops_from_min": round(2.0 * A.nnz / vals["TimeMin"] * 1e-9, 3),
-            "time_min_s": vals["TimeMin"], "time_avg_s": vals["TimeAvg"],
-            "time_max_s": vals.get("TimeMax"),
-            "sample": (f"the reference's spmv-csr main (oracle/_ref, built from spmv-csr/spmv.c) on "
-                       f"the C2 matrix in fp32 (its only dtype), x = 1, num_runs = {runs}, "
-                       f"OMP_SCHEDULE=static")}
+            "value": round(2.0 * A.nnz / tmin * 1e-9, 3), "unit": "GFLOP/s",
+            "gflops_from_avg": round(2.0 * A.nnz / tavg * 1e-9, 3),
+            "time_min_s": tmin, "time_avg_s": tavg, "time_max_s": max(ts), "runs": len(ts),
+            "sample": (f"the reference's omp_spmv (oracle/_ref, built from spmv-csr/spmv.c) on the "
+                       f"same matrix in fp32, OMP_SCHEDULE=static, {threads} threads, 5 warm-ups + "
+                       f"{len(ts)} timed calls, value = 2 nnz / TimeMin")}
 
+
+# ------------------------------------------------------------------ main
 
 def main():
     args = parse()
+    if args.dry_run:
+        dry_run(args)
+        return
+    import torch  # device memory, streams, torch.distributed: plumbing
+
+    import hspmv
+    from hspmv import dist as hdist
+    from hspmv import gen
+
     rank, world, local = dist_setup(args)
-    dtype = np.float64
-    shard = hdist.build_shard(args.config, rank, world, dtype)
-    A = shard.A
+    cfg = resolve_config(args)
+    shard = hdist.build_shard(cfg, rank, world)
+    A, maps = shard.A, shard.maps
+    np_dt = A.val.dtype
+    tdt = torch.float64 if np_dt == np.float64 else torch.float32
     # one non-default stream for everything: the SpMV launches (through the C
-    # ABI), the flush writes and the timing events all live on it
+    # ABI), the flush reads and the timing events all live on it
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
-    op = hspmv.SpMV(A, device=local, stream=stream.cuda_stream, kernel=args.kernel,
+    op = hspmv.SpMV(A, maps, device=local, stream=stream.cuda_stream, kernel=args.kernel,
                     lanes=args.lanes, nontemporal=args.nt)
     info = op.info
 
     # x: generated on rank 0, broadcast over RCCL (the path's exchange step)
-    x = torch.empty(shard.n_global, dtype=torch.float64, device="cuda")
+    x = torch.empty(shard.n_global, dtype=tdt, device="cuda")
     if rank == 0:
-        x.copy_(torch.from_numpy(gen.rand_x(shard.n_global, 42)))
+        x.copy_(torch.from_numpy(gen.rand_x(shard.n_global, 42, dtype=np_dt)))
     barrier(world)
     t0 = time.perf_counter()
     if world > 1:
         hdist.broadcast_x(x)
     barrier(world)
     bcast_ms = (time.perf_counter() - t0) * 1e3
-    y = torch.empty(A.m, dtype=torch.float64, device="cuda")
+    y = torch.empty(A.m, dtype=tdt, device="cuda")
     op.bind_x_device(x.data_ptr())
     op.bind_y_device(y.data_ptr())
 
-    # warmup
     for _ in range(args.warmup):
         op.spmv()
     barrier(world)
 
-    # timed region: exactly K steps
+    # timed region: exactly K steps; HIP events on the launch stream bracket
+    # the same K SpMVs (the kernel-side time of one SpMV = their average)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
     t0 = time.perf_counter()
@@ -236,30 +324,29 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     barrier(world)
-    step_s = max_over_ranks(wall / args.steps, world)
-    ev_launch_s = ev0.elapsed_time(ev1) * 1e-3 / args.steps  # avg launch on this stream
+    step_s = reduce_over_ranks(wall / args.steps, world, "max")
+    ev_launch_s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
 
     # cold: evict the 256 MiB Infinity Cache before every launch by READING a
     # 512 MiB buffer (a read leaves no dirty lines whose write-back the SpMV
     # would then pay for)
     flush = torch.ones(64 << 20, dtype=torch.float64, device="cuda")
-    sink = torch.empty(1, dtype=torch.float64, device="cuda")
     cold = []
     for _ in range(args.cold_steps):
-        torch.sum(flush, dim=0, out=sink)
+        flush.sum()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
         op.spmv()
         b.record(stream)
         torch.cuda.synchronize()
         cold.append(a.elapsed_time(b) * 1e-3)
-    del flush, sink
-    cold_s = max_over_ranks(float(np.median(cold)), world)
+    del flush
+    cold_s = reduce_over_ranks(float(np.median(cold)), world, "max") if cold else None
 
     # correctness property on the last y (no oracle in the product bench)
-    y_host = y.cpu().numpy()
-    ok, rel = hdist.checksum_ok(A, x.cpu().numpy(), y_host)
-    ok_all = sum_over_ranks(1.0 if ok else 0.0, world) == world
+    x_host = x.cpu().numpy()
+    ok, rel = hdist.checksum_ok(A, x_host, y.cpu().numpy())
+    ok_all = reduce_over_ranks(1.0 if ok else 0.0, world, "sum") == world
 
     # exchange step costs (reported, not in the step): y all-gather over RCCL,
     # and the halo exchange that replaces the x broadcast when x is
@@ -275,7 +362,7 @@ def main():
             barrier(world)
             times.append((time.perf_counter() - t0) * 1e3)
             del yfull
-        gather_ms = max_over_ranks(float(np.median(times)), world)
+        gather_ms = reduce_over_ranks(float(np.median(times)), world, "max")
         halo = hdist.plan_halo(A, shard.splits, rank, world)
         xw = x[halo.lo:halo.hi].clone()
         times = []
@@ -285,26 +372,30 @@ def main():
             hdist.halo_exchange(xw, halo)
             torch.cuda.synchronize()
             times.append((time.perf_counter() - t0) * 1e3)
-        halo_ms = max_over_ranks(float(np.median(times)), world)
-        halo_b = int(max_over_ranks(float(hdist.halo_bytes(halo)), world))
+        halo_ms = reduce_over_ranks(float(np.median(times)), world, "max")
+        halo_b = int(reduce_over_ranks(float(hdist.halo_bytes(halo, x.element_size())), world, "max"))
         halo_ok = bool(torch.equal(xw, x[halo.lo:halo.hi]))
-        ok_all = ok_all and sum_over_ranks(1.0 if halo_ok else 0.0, world) == world
+        ok_all = ok_all and reduce_over_ranks(1.0 if halo_ok else 0.0, world, "sum") == world
         del xw
 
     flops_step = 2.0 * shard.nnz_global
     alg_local = info["alg_bytes"]  # x counted as the distinct columns this shard reads
-    alg_total = sum_over_ranks(alg_local, world)
+    alg_total = reduce_over_ranks(alg_local, world, "sum")
     gflops = flops_step / step_s * 1e-9
     achieved = alg_local / ev_launch_s * 1e-9
-    workload_key = f"{args.config}-w{world}-r0-{info['kernel_name']}"
+    workload_key = f"{cfg}-w{world}-r0-{info['kernel_name']}"
     traffic = load_traffic(workload_key) if rank == 0 else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(A, x.cpu().numpy(), args.cpu_seconds)
-        cpu["reference_f32"] = reference_cpu(A)
+        cpu, threads = cpu_baseline(A, x_host, args.cpu_seconds)
+        cpu["reference_f32"] = reference_cpu(A, x_host, threads, 0.5 * args.cpu_seconds)
 
     if rank == 0:
+        ctype = "double" if np_dt == np.float64 else "float"
+        kname = {"csr3": "hspmv_csr3", "stream": "hspmv_csr_stream",
+                 "vector": "hspmv_csr_vector"}.get(info["kernel_name"], info["kernel_name"])
+        launches = info["x_slabs"] or 1
         out = {
             "metric": METRIC,
             "value": round(gflops, 3),
@@ -316,30 +407,40 @@ def main():
             "higher_is_better": True,
             "scaling": shard.scaling,
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f64" if np_dt == np.float64 else "f32",
             "data": "synthetic (seeded generator, hspmv.gen); x = rand_x(n, 42)",
-            "config": {"workload": f"{args.config}: {shard.name}", "m": shard.m_global,
-                       "nnz": shard.nnz_global, "rows_per_gpu": int(A.m),
-                       "kernel": info["kernel_name"], "lanes": info["lanes"],
+            "config": {"workload": f"{cfg}: {shard.name}", "m": shard.m_global,
+                       "nnz": shard.nnz_global, "rows_per_gpu": int(A.m), "nnz_per_gpu": int(A.nnz),
+                       "csr3_maps": ({"n_ssr": maps.n_ssr, "n_sr": maps.n_sr} if maps is not None
+                                     else None),
+                       "kernel": info["kernel_name"], "chunk_u": info["chunk_u"],
+                       "x_dict": info["x_dict"], "x_windows": info["x_windows"],
+                       "x_slabs": info["x_slabs"], "col16": info["col16"],
                        "nontemporal": bool(args.nt), "parallelism": f"row-range x{world}",
-                       "workload_key": workload_key, "col16": info["col16"]},
+                       "workload_key": workload_key},
             "gbps_alg": round(alg_total / step_s * 1e-9, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": (traffic["hbm_bytes_per_launch"] if traffic else None),
-                         "kernel": f"hspmv_csr_{info['kernel_name']}<double>",
+                         "kernel": f"{kname}<{ctype},...>",
+                         "row_kernel_launches_per_spmv": launches,
+                         "split_row_launches_per_spmv": 2 if info["n_split_rows"] else 0,
                          "alg_bytes_per_launch": alg_local,
                          "format_bytes_per_launch": info["format_bytes"],
                          "launch_us_events": round(ev_launch_s * 1e6, 3),
-                         "traffic_source": (traffic["source"] if traffic else None)},
-            "cold": {"launch_us": round(cold_s * 1e6, 3),
-                     "gbps_alg": round(alg_local / cold_s * 1e-9, 2),
-                     "gflops": round(flops_step / cold_s * 1e-9, 3),
-                     "note": "a 512 MiB read before each launch evicts the Infinity Cache"},
+                         "traffic_source": (traffic["file"] + ": " + traffic["source"]
+                                            if traffic else None)},
+            "cold": ({"launch_us": round(cold_s * 1e6, 3),
+                      "gbps_alg": round(alg_local / cold_s * 1e-9, 2),
+                      "frac": round(alg_local / cold_s * 1e-9 / HBM_PEAK_GBS, 4),
+                      "gflops": round(2.0 * A.nnz / cold_s * 1e-9, 3),
+                      "note": "a 512 MiB read before each launch evicts the Infinity Cache"}
+                     if cold_s else None),
             "comm": {"bcast_x_ms": round(bcast_ms, 3) if world > 1 else None,
                      "gather_y_ms": round(gather_ms, 3) if gather_ms is not None else None,
                      "halo_x_ms": round(halo_ms, 4) if halo_ms is not None else None,
-                     "x_bytes": shard.n_global * 8, "y_bytes": shard.m_global * 8,
+                     "x_bytes": shard.n_global * x.element_size(),
+                     "y_bytes": shard.m_global * x.element_size(),
                      "halo_bytes_per_rank": halo_b if world > 1 else None,
                      "end_to_end_gflops": (round(flops_step / (step_s + gather_ms * 1e-3) * 1e-9, 3)
                                            if gather_ms is not None else round(gflops, 3)),
@@ -351,6 +452,7 @@ def main():
         print(json.dumps(out), flush=True)
     op.close()
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
     if not ok_all:
         sys.exit(3)

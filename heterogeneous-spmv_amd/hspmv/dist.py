@@ -27,11 +27,12 @@ matrix.
 from __future__ import annotations
 
 from dataclasses import dataclass
+from typing import Optional
 
 import numpy as np
 
 from . import gen
-from .api import CsrMatrix, partition_rows
+from .api import CsrMatrix, Csr3Maps, build_csr3_maps, csr3_params, partition_rows
 
 
 # ------------------------------------------------------------------ workloads
@@ -47,6 +48,57 @@ class Shard:
     world: int
     name: str
     scaling: str          # "weak" (per-rank work fixed) or "strong"
+    maps: Optional[Csr3Maps] = None  # CSR-3 maps of this rank's rows (rebased)
+
+
+# The BASELINE.json configurations a bench / test run can name.
+#   c2  configs[1]  CSR fp64, 5-pt Laplacian 1000^2 per rank (weak)
+#   c3  configs[2]  CSR-3 fp64, 27-pt 125^3 RCM, (ssrs, srs) = (20, 10) from
+#                   the .csr3 writer heuristic (reformat-csr-to-csr3/spmv-auto.cpp:154-173)
+#   c3h configs[2]  alt: hugebubbles-00000 stand-in, CSR fp64
+#   c4  configs[3]  CSR fp64, banded m = 2e7 split over the ranks (strong)
+#   c5  configs[4]  CSR-3 fp32, power-law m = 2e6 (MI355X grouping)
+CONFIGS = ("c2", "c3", "c3h", "c4", "c5")
+
+
+def default_config(world: int) -> str:
+    """N = 1: C3, the largest single-GPU configuration (BASELINE.json
+    configs[2]); N > 1: C4, the configuration the multi-GPU target is stated
+    on (configs[3], row-range partition of one 200 M-nnz matrix)."""
+    return "c3" if world == 1 else "c4"
+
+
+def slice_csr3(A: CsrMatrix, maps: Csr3Maps, splits: np.ndarray, rank: int):
+    """Rows [splits[rank], splits[rank+1]) of a CSR-3 matrix whose splits fall
+    on super-super-row boundaries (hspmv_partition_rows with maps), with the
+    matching slice of the maps rebased to the shard."""
+    r0, r1 = int(splits[rank]), int(splits[rank + 1])
+    A_loc = A.rows(r0, r1)
+    sr_first = maps.inner[maps.outer[:-1]]          # first row of every SSR
+    s0 = int(np.searchsorted(sr_first, r0, side="left"))
+    s1 = int(np.searchsorted(sr_first, r1, side="left")) if r1 < A.m else maps.n_ssr
+    outer = maps.outer[s0:s1 + 1]
+    inner = maps.inner[int(outer[0]):int(outer[-1]) + 1] - r0
+    return A_loc, Csr3Maps(outer - outer[0], inner)
+
+
+def _whole_matrix(config: str, dtype):
+    if config == "c3":
+        A = gen.stencil27(125, dtype=dtype)
+        return A, build_csr3_maps(A, *csr3_params(A.nnz / A.m, "volta")), \
+            "27-pt stencil 125^3 RCM (fp64 CSR-3, ssrs=20, srs=10)"
+    if config == "c3h":
+        A = gen.honeycomb(4280, 4280, dtype=dtype)
+        return A, None, "hugebubbles-00000 stand-in: honeycomb 4280^2 RCM (fp64 CSR)"
+    if config == "c5":
+        A = gen.powerlaw(2_000_000, seed=1234, dtype=dtype)
+        return A, build_csr3_maps(A, *csr3_params(A.nnz / A.m, "mi355x")), \
+            "power-law m=2e6, Pareto alpha=1.5, seed 1234 (fp32 CSR-3)"
+    raise ValueError(config)
+
+
+def config_dtype(config: str):
+    return np.float32 if config == "c5" else np.float64
 
 
 def laplace2d_row_nnz(nx: int, ny: int) -> np.ndarray:
@@ -79,11 +131,46 @@ def splits_from_row_nnz(row_nnz: np.ndarray, world: int) -> np.ndarray:
     return partition_rows(rp.astype(np.int32), world)
 
 
-def build_shard(config: str, rank: int, world: int, dtype=np.float64) -> Shard:
+def plan_splits(config: str, world: int) -> dict:
+    """The row partition a run of `config` on `world` ranks uses, from row
+    lengths alone (no matrix, no GPU): what ``bench.py --dry-run`` prints.
+    Only the configurations whose row lengths are known in closed form."""
+    if config in ("c2", "small"):
+        nx = 1000 if config == "c2" else 64
+        row_nnz = laplace2d_row_nnz(nx, nx * world)
+        scaling = "weak"
+    elif config == "c4":
+        row_nnz = banded_row_nnz(20_000_000)
+        scaling = "strong"
+    else:
+        raise ValueError(f"no closed-form row lengths for {config!r}")
+    s = splits_from_row_nnz(row_nnz, world)
+    rp = np.zeros(row_nnz.shape[0] + 1, np.int64)
+    np.cumsum(row_nnz, out=rp[1:])
+    return {"config": config, "world": world, "scaling": scaling, "m": int(row_nnz.shape[0]),
+            "nnz": int(rp[-1]), "splits": [int(v) for v in s],
+            "rows_per_rank": [int(v) for v in np.diff(s)],
+            "nnz_per_rank": [int(v) for v in rp[s[1:]] - rp[s[:-1]]]}
+
+
+def build_shard(config: str, rank: int, world: int, dtype=None) -> Shard:
     """c2: 5-pt Laplacian, 1000 x 1000 rows per rank (global grid 1000 x 1000*world,
            weak scaling; world = 1 is BASELINE configs[1] exactly).
+       c3 / c3h / c5: one matrix (configs[2], configs[4]) split over the
+           ranks, nnz-balanced on super-super-row boundaries when it has
+           CSR-3 maps (strong scaling; every rank generates the whole matrix
+           and keeps its rows).
        c4: banded m = 2e7 (BASELINE configs[3]) split over the ranks (strong).
        small: 5-pt Laplacian 64 x 64 per rank (tests)."""
+    dtype = config_dtype(config) if dtype is None else dtype
+    if config in ("c3", "c3h", "c5"):
+        A, maps, name = _whole_matrix(config, dtype)
+        splits = partition_rows(A.row_ptr, world, maps)
+        if maps is not None:
+            A_loc, m_loc = slice_csr3(A, maps, splits, rank)
+        else:
+            A_loc, m_loc = A.rows(int(splits[rank]), int(splits[rank + 1])), None
+        return Shard(A_loc, A.n, A.m, A.nnz, splits, rank, world, name, "strong", m_loc)
     if config in ("c2", "small"):
         nx = 1000 if config == "c2" else 64
         ny = nx * world

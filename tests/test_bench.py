@@ -1,14 +1,70 @@
-"""bench.py contract on one GPU: one JSON line with the driver's keys, the
-roofline and cpu_baseline objects, and a passing y check (short run)."""
+"""bench.py contract: the CPU-side dry run names the configuration each world
+size measures (C3 at N = 1, C4 strong scaling at N > 1) and its partition;
+on one GPU, one JSON line with the driver's keys, the roofline and
+cpu_baseline objects, and a passing y check (short run)."""
 import json
 import os
 import subprocess
 import sys
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 REPO = Path(__file__).resolve().parents[1]
+
+
+def _dry(*args):
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--dry-run", *args], cwd=REPO,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    return json.loads(lines[0])
+
+
+def test_dry_run_n1_is_c3():
+    d = _dry()
+    assert d["n_gpus"] == 1 and d["config"] == "c3"
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_dry_run_multi_gpu_is_c4_strong_nnz_balanced(n):
+    d = _dry("--gpus", str(n))
+    assert d["config"] == "c4"
+    p = d["plan"]
+    assert p["scaling"] == "strong" and p["world"] == n and p["m"] == 20_000_000
+    assert len(p["splits"]) == n + 1 and p["splits"][0] == 0 and p["splits"][-1] == p["m"]
+    assert sum(p["nnz_per_rank"]) == p["nnz"] and 199_999_000 < p["nnz"] <= 200_000_000
+    assert max(p["nnz_per_rank"]) - min(p["nnz_per_rank"]) <= 20
+
+
+def test_bench_rejects_bad_arguments():
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "0", "--dry-run"],
+                         cwd=REPO, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "--gpus" in out.stderr
+
+
+def test_c3_shards_cover_the_matrix_on_ssr_boundaries():
+    """A CSR-3 configuration split over ranks keeps whole super-super-rows
+    per rank and every row exactly once (what bench.py --config c3 --gpus N
+    gives each rank); checked on a small CSR-3 matrix with the same code."""
+    from hspmv import dist as hdist
+    from hspmv import gen
+    import hspmv
+    A = gen.laplace2d(40, 30)
+    maps = hspmv.build_csr3_maps(A, 7, 8)
+    for world in (1, 2, 3, 5):
+        splits = hspmv.partition_rows(A.row_ptr, world, maps)
+        rows = 0
+        for r in range(world):
+            A_loc, m_loc = hdist.slice_csr3(A, maps, splits, r)
+            assert m_loc.inner[0] == 0 and m_loc.inner[-1] == A_loc.m
+            assert m_loc.outer[0] == 0 and m_loc.outer[-1] == m_loc.n_sr
+            assert np.array_equal(A_loc.col_idx,
+                                  A.col_idx[A.row_ptr[splits[r]]:A.row_ptr[splits[r + 1]]])
+            rows += A_loc.m
+        assert rows == A.m
 
 
 @pytest.mark.gpu
@@ -16,7 +72,7 @@ def test_bench_json_line_contract():
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--steps", "20", "--warmup", "3",
                           "--cold-steps", "2", "--cpu-seconds", "0.5"],
-                         cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+                         cwd=REPO, env=env, capture_output=True, text=True, timeout=400)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
@@ -27,13 +83,18 @@ def test_bench_json_line_contract():
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 20 and d["warmup"] == 3
     assert d["unit"] == "GFLOP/s" and d["value"] > 0 and d["higher_is_better"] is True
-    assert d["dtype"] == "f64" and d["config"]["workload"].startswith("c2")
+    assert d["dtype"] == "f64" and d["config"]["workload"].startswith("c3")
+    assert d["config"]["kernel"] == "csr3" and d["config"]["nnz"] == 51_895_117
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert r["kernel"].startswith("hspmv_csr3<double")
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
-    ref = c["reference_f32"]  # the reference's own program, when oracle/_ref was built
+    assert abs(c["value"] - 2 * d["config"]["nnz"] / c["time_min_s"] * 1e-9) < 1e-2 * c["value"]
+    assert "nnz=51895117" in c["sample"]
+    ref = c["reference_f32"]  # the reference's own omp_spmv, when oracle/_ref was built
     if (REPO / "oracle" / "_ref" / "libref_spmvcsr.so").exists():
-        assert ref["kind"] == "reference" and ref["value"] > 0 and ref["time_avg_s"] > 0
+        assert ref["kind"] == "reference" and ref["value"] > 0 and ref["time_min_s"] > 0
+    assert d["cold"]["launch_us"] > 0
     assert d["check"]["pass"] is True
