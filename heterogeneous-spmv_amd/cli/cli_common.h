@@ -7,15 +7,17 @@
 //           spmv-csr/spmv.c:164-185, hip/spmv-auto-mi100.cu:200-240) and
 //           "Number Wrong: %d" (|y - yhat| > 0.01 against a serial CPU SpMV,
 //           cuda-spmv-csr/spmv.cu:270-284), parsed by run_scripts/run_norm.py:94-107.
-// plus extra lines: KernelMin/KernelAvg (HIP-event device time), GFLOPs, GBps
-// (algorithmic bytes / KernelMin), NumGPUs, Kernel, and "Check: PASS|FAIL
-// maxrel=..." (1e-6 relative fp64 tolerance with an absolute floor).
+// plus extra lines: KernelMin/KernelAvg (HIP-event device time), GFLOPs and
+// GBps (2 nnz and algorithmic bytes / TimeMin, the wall time printed above),
+// KernelGFLOPs/KernelGBps (the same / KernelMin), NumGPUs, Kernel, and
+// "Check: PASS|FAIL maxrel=..." (1e-6 relative fp64 tolerance with an
+// absolute floor).
 //
 // Options (after the positional arguments):
 //   --gpus N            row-range partition over N GPUs (RCCL x-bcast / y-gather)
 //   --dtype f32|f64     value type (default f64; f32 = the reference's type)
 //   --x ones|rand:SEED  input vector (default ones, as the reference)
-//   --kernel auto|stream|vector[:L]|csr3
+//   --kernel auto|stream|vector[:L]|csr3|csort
 //   --nt                non-temporal loads of the matrix streams
 //   --dump-y PATH       write y as raw binary (dtype) for external checks
 //   --no-check          skip the serial CPU check
@@ -81,6 +83,7 @@ inline bool parse_options(int argc, char **argv, int first, Options &o) {
       if (!strcmp(v, "auto")) o.kernel = HSPMV_KERNEL_AUTO;
       else if (!strcmp(v, "stream")) o.kernel = HSPMV_KERNEL_STREAM;
       else if (!strcmp(v, "csr3")) o.kernel = HSPMV_KERNEL_CSR3;
+      else if (!strcmp(v, "csort")) o.kernel = HSPMV_KERNEL_CSORT;
       else if (!strncmp(v, "vector", 6)) {
         o.kernel = HSPMV_KERNEL_VECTOR;
         if (v[6] == ':') o.lanes = (unsigned)atoi(v + 7);
@@ -195,12 +198,17 @@ inline int run_and_report(const hspmv_csr_buf &A, const hspmv_csr3_buf *maps, in
   printf("TimeAvg: %lg\n", t.wall_avg);
   printf("KernelMin: %lg\n", t.t_min);
   printf("KernelAvg: %lg\n", t.t_avg);
-  printf("GFLOPs: %lg\n", t.gflops);
-  printf("GBps: %lg\n", t.gbps_alg);
+  // GFLOPs / GBps from TimeMin, as a run_scripts consumer computes them
+  // (run_norm.py:94-107 records TimeMin); the HIP-event rates beside them
+  printf("GFLOPs: %lg\n", t.wall_min > 0 ? 2.0 * (double)A.nnz / t.wall_min * 1e-9 : 0.0);
+  printf("GBps: %lg\n", t.wall_min > 0 ? info.alg_bytes / t.wall_min * 1e-9 : 0.0);
+  printf("KernelGFLOPs: %lg\n", t.gflops);
+  printf("KernelGBps: %lg\n", t.gbps_alg);
   printf("NumGPUs: %d\n", t.num_gpus);
-  static const char *kname[] = {"auto", "vector", "stream", "csr3"};
+  static const char *kname[] = {"auto", "vector", "stream", "csr3", "csort"};
   printf("Kernel: %s lanes=%d waves_per_block=%d blocks=%lld\n",
-         kname[info.kernel & 3], info.lanes, info.waves_per_block, (long long)info.blocks);
+         kname[(info.kernel >= 0 && info.kernel <= 4) ? info.kernel : 0], info.lanes,
+         info.waves_per_block, (long long)info.blocks);
   const size_t sv = A.dtype == HSPMV_F64 ? 8 : 4;
   std::vector<char> y(sv * (size_t)(A.m ? A.m : 1));
   if (hspmv_get_y(h, y.data()) != HSPMV_OK) return die("hspmv_get_y");

@@ -1,0 +1,176 @@
+// csort.hip -- the column-sorted row-block kernel (HSPMV_KERNEL_CSORT) for
+// matrices whose gathers are irregular (power-law / random columns, C5).
+//
+// Why: with random columns every nonzero of the row kernels is its own L2
+// request (one 4-8 B x entry per 128 B line), and C5's 48 M gathers hit the
+// L2 request rate (x slabs: 4 passes x 12.6 M TCC requests, TCC busy 83 %,
+// profiles/r01_pmc_c5_slabs).  Here each workgroup owns a nnz-balanced block
+// of rows and one of H column parts, and walks the block's nonzeros IN
+// COLUMN ORDER: the 64 lanes of a gather then fall on a few x lines (one
+// request serves several lanes) and all CUs of an XCD sweep x together, so
+// the lines they fetch are L2 hits for each other.  Workgroup b = (row block
+// b / H, column part b % H); under round-robin dispatch the parts alternate
+// XCDs, so each XCD's L2 only ever holds its part of x.  Probe:
+// profiles/r02*_c5_csort_probe.jsonl (C5: 264 us library -> 109 us).
+//
+// Row sums: one fp64 LDS slot per row of the block (plus one per long-row
+// slice and a dummy slot for padding), accumulated with ds_add_f64.  The
+// products are formed exactly as omp_spmv forms them for fp64 (v*x rounded),
+// and exactly (fp32 x fp32 in fp64) for fp32; the fp64 sums are rounded to
+// the value type once.  The order of the additions is the atomic order, so
+// unlike the STREAM/CSR3 kernels this path is NOT bitwise equal to omp_spmv:
+// fp32 results are more accurate than omp_spmv's fp32 running sum (and equal
+// run to run except where an fp64 sum sits within an fp64 rounding of an
+// fp32 tie), fp64 results agree with it to the fp64 rounding of the sum.
+//
+// Layout (built on the host, hspmv_api.cpp build_csort): entries padded to
+// whole chunks of 64*U; per chunk a base column (cbase); per entry idx =
+// slot << 16 | (col - base) (a chunk never spans more than 65535 columns)
+// and the value: fp32 as one 8-byte {idx, val} record (one load per
+// element), fp64 as idx[] + val[].  The fp64 partial sums of the H parts
+// (part[h * m + row]) and of the long-row slices (spart[slice]) are combined
+// in a fixed order by hspmv_csort_finish.
+#include <hip/hip_runtime.h>
+
+#include "hspmv_internal.h"
+
+namespace hspmv {
+namespace {
+
+constexpr int kWave = 64;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+template <bool NT, typename P>
+__device__ __forceinline__ P ld(const P *p) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+
+__device__ __forceinline__ int32_t wave_uniform(int32_t v) {
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+template <typename T, int U, bool NT>
+__global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
+    int32_t H, int64_t m, int32_t direct, const int32_t *__restrict__ blk_c,
+    const int32_t *__restrict__ blk_r, const int32_t *__restrict__ blk_v,
+    const int32_t *__restrict__ vslice, const int32_t *__restrict__ cbase,
+    const void *__restrict__ ent, const T *__restrict__ val, const T *__restrict__ x,
+    double *__restrict__ part, double *__restrict__ spart, T *__restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double *acc = reinterpret_cast<double *>(smem);
+  constexpr int NW = kCsortThreads / kWave;
+  const int b = blockIdx.x;
+  const int rb = b / H, h = b - rb * H;
+  const int32_t c0 = blk_c[b], c1 = blk_c[b + 1];
+  const int32_t r0 = blk_r[rb], r1 = blk_r[rb + 1];
+  const int32_t v0 = blk_v[b], v1 = blk_v[b + 1];
+  const int32_t nr = r1 - r0, nv = v1 - v0;
+  for (int32_t i = threadIdx.x; i <= nr + nv; i += kCsortThreads) acc[i] = 0.0;  // + dummy
+  __syncthreads();
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+  for (int32_t c = c0 + wid; c < c1; c += NW) {  // wave-uniform
+    const int32_t base = wave_uniform(cbase[wave_uniform(c)]);
+    const int64_t k0 = (int64_t)c * (kWave * U) + lane;
+    uint32_t ix[U];
+    T vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (sizeof(T) == 4) {
+        const u32x2 p = ld<NT>(reinterpret_cast<const u32x2 *>(ent) + k0 + u * kWave);
+        ix[u] = p.x;
+        vv[u] = __uint_as_float(p.y);
+      } else {
+        ix[u] = ld<NT>(reinterpret_cast<const uint32_t *>(ent) + k0 + u * kWave);
+        vv[u] = ld<NT>(val + k0 + u * kWave);
+      }
+    }
+    T xv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xv[u] = x[base + (int32_t)(ix[u] & 0xffffu)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      double pr;
+      if constexpr (sizeof(T) == 4)
+        pr = (double)vv[u] * (double)xv[u];  // exact
+      else
+        pr = (double)(vv[u] * xv[u]);  // omp_spmv's rounded product
+      atomicAdd(&acc[ix[u] >> 16], pr);
+    }
+  }
+  __syncthreads();
+  if (direct) {  // one column part, no long rows: y straight from the slots
+    for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) y[r0 + i] = (T)acc[i];
+    return;
+  }
+  double *out = part + (int64_t)h * m + r0;
+  for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) out[i] = acc[i];
+  for (int32_t i = threadIdx.x; i < nv; i += kCsortThreads) spart[vslice[v0 + i]] = acc[nr + i];
+}
+
+// y[r] = part[r] + part[m + r] + ... (parts in order), except long rows:
+// blocks past the row blocks sum each long row's slices (one wave per row,
+// fixed lane assignment and shuffle tree).
+template <typename T>
+__global__ __launch_bounds__(256) void hspmv_csort_finish(
+    int64_t m, int32_t H, int64_t row_blocks, const double *__restrict__ part,
+    const uint32_t *__restrict__ long_mask, int32_t n_long, const int32_t *__restrict__ long_row,
+    const int32_t *__restrict__ long_cs, const double *__restrict__ spart, T *__restrict__ y) {
+  if ((int64_t)blockIdx.x < row_blocks) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= m) return;
+    if (long_mask && ((long_mask[r >> 5] >> (r & 31)) & 1u)) return;
+    double s = part[r];
+    for (int32_t h = 1; h < H; ++h) s += part[(int64_t)h * m + r];
+    y[r] = (T)s;
+    return;
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t j = ((int64_t)blockIdx.x - row_blocks) * 4 + (threadIdx.x >> 6);
+  if (j >= n_long) return;
+  double s = 0.0;
+  for (int32_t i = long_cs[j] + lane; i < long_cs[j + 1]; i += kWave) s += spart[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
+  if (lane == 0) y[long_row[j]] = (T)s;
+}
+
+template <typename T, int U, bool NT>
+hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
+  hipLaunchKernelGGL((hspmv_csort<T, U, NT>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
+                     (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
+                     c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, c.part, c.spart, y);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || c.direct) return e;
+  const int64_t rb = (c.m + 255) / 256;
+  const int64_t lb = ((int64_t)c.n_long + 3) / 4;
+  hipLaunchKernelGGL((hspmv_csort_finish<T>), dim3((unsigned)(rb + lb)), dim3(256), 0, st, c.m,
+                     c.H, rb, c.part, c.long_mask, c.n_long, c.long_row, c.long_cs, c.spart, y);
+  return hipGetLastError();
+}
+
+template <typename T, bool NT>
+hipError_t launch_csort_nt(const DevCsort &c, const T *x, T *y, hipStream_t st) {
+  switch (c.u) {
+    case 4: return launch_csort_u<T, 4, NT>(c, x, y, st);
+    case 8: return launch_csort_u<T, 8, NT>(c, x, y, st);
+    case 16: return launch_csort_u<T, 16, NT>(c, x, y, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_csort(const DevCsort &c, int dtype, const void *x, void *y, hipStream_t st) {
+  if (c.m == 0) return hipSuccess;
+  if (c.n_wg <= 0 || c.lds_bytes > kCsortMaxLds) return hipErrorInvalidValue;
+  if (dtype == 1)
+    return c.nontemporal ? launch_csort_nt<double, true>(c, (const double *)x, (double *)y, st)
+                         : launch_csort_nt<double, false>(c, (const double *)x, (double *)y, st);
+  return c.nontemporal ? launch_csort_nt<float, true>(c, (const float *)x, (float *)y, st)
+                       : launch_csort_nt<float, false>(c, (const float *)x, (float *)y, st);
+}
+
+}  // namespace hspmv

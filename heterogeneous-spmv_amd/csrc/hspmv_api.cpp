@@ -66,6 +66,16 @@ struct Shard {
   int32_t *d_slab_col = nullptr;     // slab-major columns and values
   void *d_slab_val = nullptr;
   int32_t n_slabs = 0;
+  // column-sorted row blocks (build_csort): owned tables, and the launch
+  // description they form (copied into dp.cs when the planner picks kCsort)
+  int32_t *d_cs_blk_c = nullptr, *d_cs_blk_r = nullptr, *d_cs_blk_v = nullptr,
+          *d_cs_vslice = nullptr, *d_cs_cbase = nullptr, *d_cs_long_row = nullptr,
+          *d_cs_long_cs = nullptr;
+  uint32_t *d_cs_mask = nullptr;
+  void *d_cs_ent = nullptr, *d_cs_val = nullptr;
+  double *d_cs_part = nullptr, *d_cs_spart = nullptr;
+  DevCsort csort;
+  double csort_format_bytes = 0.0;   // bytes one csort SpMV moves
   int c16g_shape = 0;                // group-base columns built for kStream groups / kCsr3 tasks
   std::vector<int32_t> h_xwin;       // built at upload (host columns at hand)
   std::vector<int32_t> h_xwin_t;     // the same per packed CSR-3 task
@@ -141,6 +151,11 @@ void free_shard(Shard &s, bool borrowed) {
   (void)hipFree(s.d_slab_rp);
   (void)hipFree(s.d_slab_col);
   (void)hipFree(s.d_slab_val);
+  for (void *p : {(void *)s.d_cs_blk_c, (void *)s.d_cs_blk_r, (void *)s.d_cs_blk_v,
+                  (void *)s.d_cs_vslice, (void *)s.d_cs_cbase, (void *)s.d_cs_long_row,
+                  (void *)s.d_cs_long_cs, (void *)s.d_cs_mask, s.d_cs_ent, s.d_cs_val,
+                  (void *)s.d_cs_part, (void *)s.d_cs_spart})
+    (void)hipFree(p);
   (void)hipFree(s.d_task);
   (void)hipFree(s.d_long_row);
   (void)hipFree(s.d_long_cstart);
@@ -633,6 +648,34 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
 // row's columns to be non-decreasing slab by slab (sorted rows; checked).
 // HSPMV_XSLABS=0 disables, =B forces B slabs; HSPMV_XSLAB_BYTES moves the
 // slab size.
+// Irregular gathers: the median 64-row group gathers over more than an
+// XCD's 4 MiB L2 of x (random / power-law columns), so nearly every gather
+// of the row kernels is its own L2 request.
+bool irregular_gathers(const int32_t *rp, const int32_t *col, int64_t m, double sv) {
+  const int64_t ng = (m + 63) / 64;
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, m / 65536));
+  std::vector<int64_t> wide((size_t)nt, 0), nonempty((size_t)nt, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t]() {
+      for (int64_t g = ng * t / nt; g < ng * (t + 1) / nt; ++g) {
+        const int64_t k0 = rp[64 * g], k1 = rp[std::min(m, 64 * g + 64)];
+        if (k1 <= k0) continue;
+        int32_t lo = col[k0], hi = col[k0];
+        for (int64_t k = k0 + 1; k < k1; ++k) {
+          lo = std::min(lo, col[k]);
+          hi = std::max(hi, col[k]);
+        }
+        ++nonempty[(size_t)t];
+        if ((double)(hi - lo + 1) * sv > 4.0 * 1024 * 1024) ++wide[(size_t)t];
+      }
+    });
+  for (auto &x : th) x.join();
+  int64_t nw = 0, ne = 0;
+  for (int t = 0; t < nt; ++t) { nw += wide[(size_t)t]; ne += nonempty[(size_t)t]; }
+  return 2 * nw > ne;
+}
+
 constexpr double kSlabBytes = 2.0 * 1024 * 1024;
 constexpr int kMaxSlabs = 32;
 
@@ -651,7 +694,6 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
   if (B < 2) return HSPMV_OK;
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
   const int64_t W = (n + B - 1) / B;  // columns per slab
-  const int64_t ng = (m + 63) / 64;
   const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, m / 65536));
   auto par = [&](auto &&body) {
     std::vector<std::thread> th;
@@ -666,24 +708,7 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
     // and each pass must stream millions of nonzeros (a launch is ~2-5 us)
     const double extra = (double)(B - 1) * (4.0 * (double)(m + 1) + 2.0 * sv * (double)m);
     if (extra > 0.25 * (double)nnz * (sv + 4.0) || (double)nnz / B < 2.0e6) return HSPMV_OK;
-    // irregular: the median 64-row group gathers over more than an L2 of x
-    std::vector<int64_t> wide((size_t)nt, 0), nonempty((size_t)nt, 0);
-    par([&](int t) {
-      for (int64_t g = ng * t / nt; g < ng * (t + 1) / nt; ++g) {
-        const int64_t k0 = rp[64 * g], k1 = rp[std::min(m, 64 * g + 64)];
-        if (k1 <= k0) continue;
-        int32_t lo = col[k0], hi = col[k0];
-        for (int64_t k = k0 + 1; k < k1; ++k) {
-          lo = std::min(lo, col[k]);
-          hi = std::max(hi, col[k]);
-        }
-        ++nonempty[(size_t)t];
-        if ((double)(hi - lo + 1) * sv > 4.0 * 1024 * 1024) ++wide[(size_t)t];
-      }
-    });
-    int64_t nw = 0, ne = 0;
-    for (int t = 0; t < nt; ++t) { nw += wide[(size_t)t]; ne += nonempty[(size_t)t]; }
-    if (2 * nw <= ne) return HSPMV_OK;
+    if (!irregular_gathers(rp, col, m, sv)) return HSPMV_OK;
   }
   // per (slab, row) segment lengths; rows must be slab-monotone
   std::vector<int32_t> srp((size_t)B * (size_t)(m + 1), 0);
@@ -738,6 +763,292 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
   return HSPMV_OK;
 }
 
+
+// Column-sorted row blocks (csort.hip; the kernel's header says why).
+// Host build: rows are cut into nnz-balanced blocks of at most
+// kCsortMaxSlots - (slices) rows, about one block per CU and column part;
+// every workgroup (block, part) gets the block's nonzeros whose column lies
+// in its part, sorted by column, plus its share of the long-row slices
+// (rows > kLongRow nonzeros, cut per part into kCsortSlice-nonzero slices
+// dealt round-robin over the blocks, each an extra LDS slot).  Entries are
+// padded to whole chunks of 64*U, and a chunk is closed early when its
+// columns would span more than 65535 (16-bit offsets from the chunk base).
+// Padding entries add 0 * x[base] to a dummy slot that is never read.
+// Auto: HBM-resident matrices with irregular gathers and x beyond an XCD's
+// L2 (the x-slab rule, which it replaces: C5 264 -> ~110 us);
+// HSPMV_KERNEL_CSORT forces it, HSPMV_CSORT=0 turns auto off,
+// HSPMV_CSORT_H = 1/2/4 sets the column parts, HSPMV_CSORT_U = 4/8/16 the
+// chunk.
+constexpr int32_t kCsortSlice = 2048;
+constexpr int32_t kCsortMaxSlots = kCsortMaxLds / 8 - 1;
+
+struct CsEnt {
+  uint32_t col, slot, k;
+  bool operator<(const CsEnt &o) const {
+    return col != o.col ? col < o.col : (slot != o.slot ? slot < o.slot : k < o.k);
+  }
+};
+
+int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
+                int64_t n, int dtype, unsigned flags) {
+  if (m == 0 || n == 0 || !val) return HSPMV_OK;
+  const int64_t nnz = rp[m];
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  int H = n >= 2 ? 2 : 1;
+  if (const char *e = getenv("HSPMV_CSORT_H")) {
+    const int v = atoi(e);
+    if (v == 1 || v == 2 || v == 4) H = (int)std::min<int64_t>(v, n);
+  }
+  int U = dtype == HSPMV_F32 ? 16 : 8;
+  if (const char *e = getenv("HSPMV_CSORT_U")) {
+    const int v = atoi(e);
+    if (v == 4 || v == 8 || v == 16) U = v;
+  }
+  const int64_t C = 64 * U;
+  const size_t sv = dtype_size(dtype);
+  const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
+  auto part_of = [&](int64_t c) { return (int)((c * H) / n); };  // c in part floor(c*H/n)
+  // long rows and their slices (per part, kCsortSlice nonzeros each)
+  std::vector<int32_t> lrow, lcs(1, 0);
+  std::vector<std::vector<uint32_t>> slice_k;  // source nonzeros per slice
+  std::vector<int> slice_part;
+  int64_t long_nnz = 0;
+  for (int64_t r = 0; r < m; ++r) {
+    const int32_t k0 = rp[r], k1 = rp[r + 1];
+    if (k1 - k0 <= long_t) continue;
+    long_nnz += k1 - k0;
+    lrow.push_back((int32_t)r);
+    std::vector<std::vector<uint32_t>> byp((size_t)H);
+    for (int32_t k = k0; k < k1; ++k) byp[(size_t)part_of(col[k])].push_back((uint32_t)k);
+    for (int h = 0; h < H; ++h)
+      for (size_t i = 0; i < byp[(size_t)h].size(); i += kCsortSlice) {
+        const size_t e = std::min(byp[(size_t)h].size(), i + kCsortSlice);
+        slice_k.emplace_back(byp[(size_t)h].begin() + (ptrdiff_t)i, byp[(size_t)h].begin() + (ptrdiff_t)e);
+        slice_part.push_back(h);
+      }
+    lcs.push_back((int32_t)slice_k.size());
+  }
+  const int64_t n_slices = (int64_t)slice_k.size();
+  // row blocks, nnz-balanced over the regular rows, capped in rows
+  const int64_t nb0 = std::max<int64_t>(1, cus / H);
+  const int64_t reserve = n_slices / nb0 + 2;
+  const int64_t row_cap = kCsortMaxSlots - 1 - reserve;
+  if (row_cap < 64) return HSPMV_OK;  // too many slices for the LDS: not this path
+  const int64_t target = std::max<int64_t>(1, (nnz - long_nnz + nb0 - 1) / nb0);
+  std::vector<int32_t> br(1, 0);
+  {
+    int64_t start = 0, acc = 0;
+    for (int64_t r = 0; r < m; ++r) {
+      if (r > start && (r - start >= row_cap || acc >= target)) {
+        br.push_back((int32_t)r);
+        start = r;
+        acc = 0;
+      }
+      const int64_t d = rp[r + 1] - rp[r];
+      acc += d > long_t ? 0 : d;
+    }
+    br.push_back((int32_t)m);
+  }
+  const int64_t NB = (int64_t)br.size() - 1;
+  const int64_t G = NB * H;
+  if (G >= INT32_MAX) return HSPMV_OK;
+  // slices dealt round-robin over the blocks of their part
+  std::vector<std::vector<int32_t>> wg_sl((size_t)G);
+  {
+    std::vector<int64_t> next((size_t)H, 0);
+    for (int64_t sl = 0; sl < n_slices; ++sl) {
+      const int h = slice_part[(size_t)sl];
+      const int64_t rb = next[(size_t)h]++ % NB;
+      wg_sl[(size_t)(rb * H + h)].push_back((int32_t)sl);
+    }
+  }
+  // per workgroup: sorted entries, chunk count (pass 1)
+  std::vector<std::vector<CsEnt>> ents((size_t)G);
+  std::vector<int64_t> nchunks((size_t)G, 0);
+  std::vector<int32_t> nslots((size_t)G, 0);
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, G / 4));
+  std::atomic<bool> too_big{false};
+  auto chunk_walk = [&](const std::vector<CsEnt> &E, auto &&emit) {
+    // chunks of C entries, closed early when the span would pass 65535
+    int64_t i = 0, cnt = 0;
+    const int64_t ne = (int64_t)E.size();
+    while (i < ne) {
+      const uint32_t c0 = E[(size_t)i].col;
+      int64_t j = i;
+      while (j < ne && j - i < C && E[(size_t)j].col - c0 <= 65535u) ++j;
+      emit(cnt, c0, i, j);
+      ++cnt;
+      i = j;
+    }
+    return cnt;
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+      th.emplace_back([&, t]() {
+        for (int64_t b = t; b < G; b += nt) {
+          const int64_t rb = b / H;
+          const int h = (int)(b % H);
+          const int32_t r0 = br[(size_t)rb], r1 = br[(size_t)rb + 1];
+          const int32_t nr = r1 - r0;
+          auto &E = ents[(size_t)b];
+          for (int32_t r = r0; r < r1; ++r) {
+            if (rp[r + 1] - rp[r] > long_t) continue;
+            for (int32_t k = rp[r]; k < rp[r + 1]; ++k)
+              if (part_of(col[k]) == h) E.push_back({(uint32_t)col[k], (uint32_t)(r - r0), (uint32_t)k});
+          }
+          const auto &sl = wg_sl[(size_t)b];
+          for (size_t v = 0; v < sl.size(); ++v)
+            for (uint32_t k : slice_k[(size_t)sl[v]])
+              E.push_back({(uint32_t)col[k], (uint32_t)(nr + (int32_t)v), k});
+          std::sort(E.begin(), E.end());
+          nslots[(size_t)b] = nr + (int32_t)sl.size() + 1;  // + the dummy slot
+          if (nslots[(size_t)b] > 65536 || (int64_t)nslots[(size_t)b] * 8 > kCsortMaxLds) too_big = true;
+          nchunks[(size_t)b] = chunk_walk(E, [](int64_t, uint32_t, int64_t, int64_t) {});
+        }
+      });
+    for (auto &x : th) x.join();
+  }
+  if (too_big) return HSPMV_OK;
+  std::vector<int32_t> blk_c((size_t)G + 1, 0), blk_v((size_t)G + 1, 0), vslice;
+  int64_t tot_chunks = 0;
+  int32_t max_slots = 1;
+  for (int64_t b = 0; b < G; ++b) {
+    blk_c[(size_t)b] = (int32_t)tot_chunks;
+    tot_chunks += nchunks[(size_t)b];
+    blk_v[(size_t)b] = (int32_t)vslice.size();
+    for (int32_t sl : wg_sl[(size_t)b]) vslice.push_back(sl);
+    max_slots = std::max(max_slots, nslots[(size_t)b]);
+  }
+  blk_c[(size_t)G] = (int32_t)tot_chunks;
+  blk_v[(size_t)G] = (int32_t)vslice.size();
+  if (tot_chunks * C >= (int64_t)1 << 40 || tot_chunks >= INT32_MAX) return HSPMV_OK;
+  const int64_t tot = tot_chunks * C;
+  // pass 2: the device arrays
+  std::vector<int32_t> cbase((size_t)std::max<int64_t>(tot_chunks, 1), 0);
+  std::vector<uint32_t> idx;
+  std::vector<uint64_t> rec;
+  std::vector<double> val64;
+  if (dtype == HSPMV_F32)
+    rec.assign((size_t)tot, 0);
+  else {
+    idx.assign((size_t)tot, 0);
+    val64.assign((size_t)tot, 0.0);
+  }
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+      th.emplace_back([&, t]() {
+        for (int64_t b = t; b < G; b += nt) {
+          auto &E = ents[(size_t)b];
+          const uint32_t dummy = (uint32_t)(nslots[(size_t)b] - 1);
+          const int64_t cfirst = blk_c[(size_t)b];
+          chunk_walk(E, [&](int64_t ci, uint32_t c0, int64_t i, int64_t j) {
+            const int64_t ch = cfirst + ci;
+            cbase[(size_t)ch] = (int32_t)c0;
+            for (int64_t q = 0; q < C; ++q) {
+              const int64_t o = ch * C + q;
+              uint32_t ix = dummy << 16;  // padding: 0 * x[base] into the dummy slot
+              const void *vp = nullptr;
+              if (i + q < j) {
+                const CsEnt &e = E[(size_t)(i + q)];
+                ix = (e.slot << 16) | (e.col - c0);
+                vp = (const char *)val + sv * (size_t)e.k;
+              }
+              if (dtype == HSPMV_F32) {
+                uint32_t vb = 0;
+                if (vp) memcpy(&vb, vp, 4);
+                rec[(size_t)o] = ((uint64_t)vb << 32) | ix;
+              } else {
+                idx[(size_t)o] = ix;
+                if (vp) memcpy(&val64[(size_t)o], vp, 8);
+              }
+            }
+          });
+          std::vector<CsEnt>().swap(E);
+        }
+      });
+    for (auto &x : th) x.join();
+  }
+  std::vector<uint32_t> mask;
+  if (!lrow.empty()) {
+    mask.assign((size_t)((m + 31) / 32), 0u);
+    for (int32_t r : lrow) mask[(size_t)r >> 5] |= 1u << (r & 31);
+  }
+  int rc;
+  auto up = [&](auto **d, const auto &h) -> int {
+    using E = typename std::decay_t<decltype(h)>::value_type;
+    const size_t bytes = sizeof(E) * std::max<size_t>(h.size(), 1);
+    int r2 = dev_alloc(d, bytes, &s.bytes);
+    if (r2) return r2;
+    if (!h.empty()) HIP_TRY(hipMemcpy(*d, h.data(), sizeof(E) * h.size(), hipMemcpyHostToDevice));
+    return HSPMV_OK;
+  };
+  if ((rc = up(&s.d_cs_blk_c, blk_c)) || (rc = up(&s.d_cs_blk_r, br)) || (rc = up(&s.d_cs_blk_v, blk_v)) ||
+      (rc = up(&s.d_cs_vslice, vslice)) || (rc = up(&s.d_cs_cbase, cbase)))
+    return rc;
+  if (dtype == HSPMV_F32) {
+    uint64_t *d = nullptr;
+    if ((rc = up(&d, rec))) return rc;
+    s.d_cs_ent = d;
+  } else {
+    uint32_t *di = nullptr;
+    double *dv = nullptr;
+    if ((rc = up(&di, idx))) return rc;
+    s.d_cs_ent = di;
+    if ((rc = up(&dv, val64))) return rc;
+    s.d_cs_val = dv;
+  }
+  const bool direct = H == 1 && lrow.empty();
+  if (!direct) {
+    if ((rc = dev_alloc(&s.d_cs_part, 8 * (size_t)H * (size_t)m, &s.bytes))) return rc;
+    if ((rc = dev_alloc(&s.d_cs_spart, 8 * (size_t)std::max<int64_t>(n_slices, 1), &s.bytes))) return rc;
+  }
+  if (!lrow.empty()) {
+    if ((rc = up(&s.d_cs_mask, mask)) || (rc = up(&s.d_cs_long_row, lrow)) || (rc = up(&s.d_cs_long_cs, lcs)))
+      return rc;
+  }
+  DevCsort &c = s.csort;
+  c = DevCsort();
+  c.n_wg = (int32_t)G;
+  c.H = H;
+  c.u = U;
+  c.direct = direct ? 1 : 0;
+  c.n_long = (int32_t)lrow.size();
+  c.nontemporal = true;  // the entry stream is read once; keep x in the caches
+  if (const char *e = getenv("HSPMV_CSORT_NT")) c.nontemporal = atoi(e) != 0;
+  c.m = m;
+  c.lds_bytes = 8 * max_slots;
+  c.blk_c = s.d_cs_blk_c;
+  c.blk_r = s.d_cs_blk_r;
+  c.blk_v = s.d_cs_blk_v;
+  c.vslice = s.d_cs_vslice;
+  c.cbase = s.d_cs_cbase;
+  c.ent = s.d_cs_ent;
+  c.val = s.d_cs_val;
+  c.part = s.d_cs_part;
+  c.spart = s.d_cs_spart;
+  c.long_mask = s.d_cs_mask;
+  c.long_row = s.d_cs_long_row;
+  c.long_cs = s.d_cs_long_cs;
+  // bytes moved: the entry stream + chunk bases + x (distinct columns) + the
+  // partial sums written and read back + y
+  const double xb = (double)s.x_entries * (double)sv;
+  s.csort_format_bytes = (double)tot * (double)(4 + sv) + 4.0 * (double)tot_chunks + xb +
+                         (direct ? 0.0 : 16.0 * (double)H * (double)m + 16.0 * (double)n_slices) +
+                         (double)sv * (double)m;
+  s.A.has_csort = true;
+  return HSPMV_OK;
+}
+
+int csort_mode() {
+  const char *e = getenv("HSPMV_CSORT");
+  return e ? atoi(e) : -1;  // -1 auto, 0 off, 1 whenever it can be built
+}
+
 // Host-side tables that need the columns (built at upload, while they are
 // at hand): the CSR-3 packed tasks, the block x dictionaries, and (without
 // dictionaries) the 16-bit column offsets and the x windows of both row
@@ -749,6 +1060,23 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
   s.h_xwin.clear();
   s.h_xwin_t.clear();
   int rc;
+  {
+    const unsigned kf = flags & 0xFu;
+    const int cm = csort_mode();
+    const double sv = (double)dtype_size(dtype);
+    const double footprint = (double)rp[m] * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv;
+    bool want = kf == kCsort || cm == 1;
+    if (!want && kf == kAuto && cm != 0 && !getenv("HSPMV_XSLABS") && footprint > kMallResident &&
+        (double)n * sv > 4.0 * 1024 * 1024)
+      want = irregular_gathers(rp, col, m, sv);
+    if (want) {
+      if ((rc = build_csort(s, rp, col, val, m, n, dtype, flags))) return rc;
+      if (s.A.has_csort) {
+        s.A.col_span_bits = 31;
+        return HSPMV_OK;
+      }
+    }
+  }
   if ((rc = build_xslabs(s, rp, col, val, m, n, dtype, flags))) return rc;
   if (s.n_slabs) {  // slab passes read 32-bit columns from global x
     s.A.col_span_bits = 31;
@@ -843,6 +1171,14 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
   const int64_t m = s.A.m;
   s.dp = DevPlan();
   int64_t long_nnz = 0;
+  if (s.plan.kernel == kCsort) {  // long rows are slices of the csort blocks
+    s.dp.cs = s.csort;
+    s.plan.blocks = s.csort.n_wg;
+    s.plan.u = s.csort.u;
+    const double alg = hspmv_alg_bytes(s.A.m, s.x_entries, s.A.nnz, dtype, 0, 0);
+    s.c16_saved = alg - s.csort_format_bytes;
+    return HSPMV_OK;
+  }
   if (s.plan.kernel != kVector && !(flags & HSPMV_FLAG_NO_SPLIT)) {
     std::vector<int32_t> lrow, lcs(1, 0), ck;
     for (int64_t r = 0; r < m; ++r) {
@@ -1395,6 +1731,8 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->x_dict = s.dp.xd_blk ? 1 : 0;
   out->x_slabs = s.dp.n_slabs;
   out->col16_group = (s.A.col16 && s.A.c16_mode == 2) ? 1 : 0;
+  out->csort_parts = s.plan.kernel == kCsort ? s.dp.cs.H : 0;
+  out->n_split_rows = s.plan.kernel == kCsort ? s.dp.cs.n_long : out->n_split_rows;
   for (auto &sh : h->shards) out->x_dict_entries += sh.dp.xd_blk ? sh.xd_entries : 0;
   return HSPMV_OK;
 }

@@ -280,10 +280,13 @@ void uncoarsen(std::vector<int32_t> &map, const std::vector<int32_t> &perm_coars
   for (size_t i = 0; i < perm_finer.size(); ++i) perm_finer[i] = old_perm[(size_t)np[i]];
 }
 
-}  // namespace
-
-extern "C" int hspmv_build_csr3_bandk(const hspmv_csr *A, int ssrs, int srs, hspmv_csr_buf *A_out,
-                                      hspmv_csr3_buf *maps_out, int32_t *perm_out) {
+// levels = 3: CSR-3 (sizes s1 then s2, two coarsenings); levels = 2: CSR-2
+// (one coarsening with s1; the maps get an identity outer level, one
+// super-row per super-super-row).  BAND_k::preprocessingForSpMV's loop runs
+// "for (i = 1; i < k; i++)" (csrk.cu:1072-1096): CSR-2 coarsens and RCMs
+// once (spmv-csrk/spmv.cpp:28 CSRK_LEVEL 2, cuda/spmv.cu:130).
+int bandk_build(const hspmv_csr *A, int levels, int ssrs, int srs, hspmv_csr_buf *A_out,
+                hspmv_csr3_buf *maps_out, int32_t *perm_out) {
   clear_error();
   if (!A_out || !maps_out) return set_error(HSPMV_E_INVALID, "NULL output");
   memset(A_out, 0, sizeof(*A_out));
@@ -307,15 +310,21 @@ extern "C" int hspmv_build_csr3_bandk(const hspmv_csr *A, int ssrs, int srs, hsp
     std::vector<int32_t> perm1, inv1, perm2, inv2;
     rcm(g1, perm1, inv1);
     renumber(g1, perm1, inv1);
-    // level 2: super-super-rows over the RCM-ordered super-rows
-    const int64_t nnz1 = (int64_t)g1.c.size();
-    const int64_t thr2 = (int64_t)(int)((int64_t)srs * nnz1 / (g1.n ? g1.n : 1));
-    hand_coarsen(g1, thr2, &map2, &g2);
-    rcm(g2, perm2, inv2);
+    if (levels == 3) {
+      // level 2: super-super-rows over the RCM-ordered super-rows
+      const int64_t nnz1 = (int64_t)g1.c.size();
+      const int64_t thr2 = (int64_t)(int)((int64_t)srs * nnz1 / (g1.n ? g1.n : 1));
+      hand_coarsen(g1, thr2, &map2, &g2);
+      rcm(g2, perm2, inv2);
+    } else {  // CSR-2: every super-row is its own super-super-row
+      g2.n = g1.n;
+      map2.resize((size_t)g1.n + 1);
+      std::iota(map2.begin(), map2.end(), 0);
+    }
     // uncoarsen: level 2 onto level 1, then level 1 onto the rows
     std::vector<int32_t> perm0((size_t)m);
     std::iota(perm0.begin(), perm0.end(), 0);
-    if (g2.n > 0) uncoarsen(map2, perm2, perm1);
+    if (levels == 3 && g2.n > 0) uncoarsen(map2, perm2, perm1);
     if (g1.n > 0) uncoarsen(map1, perm1, perm0);
     // reorderA: symmetric permutation, columns sorted per row
     std::vector<int32_t> fwd((size_t)m);
@@ -365,4 +374,16 @@ extern "C" int hspmv_build_csr3_bandk(const hspmv_csr *A, int ssrs, int srs, hsp
     return set_error(HSPMV_E_NOMEM, "out of host memory");
   }
   return HSPMV_OK;
+}
+
+}  // namespace
+
+extern "C" int hspmv_build_csr3_bandk(const hspmv_csr *A, int ssrs, int srs, hspmv_csr_buf *A_out,
+                                      hspmv_csr3_buf *maps_out, int32_t *perm_out) {
+  return bandk_build(A, 3, ssrs, srs, A_out, maps_out, perm_out);
+}
+
+extern "C" int hspmv_build_csr2_bandk(const hspmv_csr *A, int srs, hspmv_csr_buf *A_out,
+                                      hspmv_csr3_buf *maps_out, int32_t *perm_out) {
+  return bandk_build(A, 2, srs, 1, A_out, maps_out, perm_out);
 }

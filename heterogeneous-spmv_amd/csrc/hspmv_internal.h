@@ -32,18 +32,40 @@ struct DevCSR {
   bool has_xwin = false, has_xdict = false;
   int32_t n_slabs = 1;        // x slabs: the row kernel's passes (each sees ~nnz / n_slabs)
   int32_t task_waves = 4;     // CSR3 packed tasks per workgroup (4, or 8 with x dictionaries)
+  bool has_csort = false;     // column-sorted row blocks were built (irregular gathers)
 };
 
 constexpr int kC16Shift = 8;  // 256 nonzeros per column-base block
 constexpr int kXWin = 256;    // largest LDS-staged x window of a row group (entries)
 
-enum Kernel : int { kAuto = 0, kVector = 1, kStream = 2, kCsr3 = 3 };
+enum Kernel : int { kAuto = 0, kVector = 1, kStream = 2, kCsr3 = 3, kCsort = 4 };
 
 // Rows longer than this many nonzeros ("split rows") are cut into chunks of
 // kLongChunk nonzeros, each summed by its own workgroup, and the chunk sums
 // are added per row by a second small kernel (deterministic order).
 constexpr int32_t kLongRow = 4096;
 constexpr int32_t kLongChunk = 4096;
+
+// Column-sorted row blocks (csort.hip): workgroup b = (row block b / H,
+// column part b % H) walks chunks [blk_c[b], blk_c[b+1]) of 64*u entries in
+// column order; its rows are [blk_r[b/H], blk_r[b/H+1]) and its long-row
+// slices vslice[blk_v[b] .. blk_v[b+1]).  Built by build_csort
+// (hspmv_api.cpp).
+constexpr int kCsortThreads = 1024;
+constexpr int kCsortMaxLds = 160 * 1024;
+struct DevCsort {
+  int32_t n_wg = 0, H = 1, u = 16, direct = 0, n_long = 0;
+  bool nontemporal = true;
+  int64_t m = 0;
+  int32_t lds_bytes = 0;
+  const int32_t *blk_c = nullptr, *blk_r = nullptr, *blk_v = nullptr, *vslice = nullptr;
+  const int32_t *cbase = nullptr;
+  const void *ent = nullptr;  // fp32: {idx, val} records; fp64: idx
+  const void *val = nullptr;  // fp64 values (nullptr for fp32)
+  double *part = nullptr, *spart = nullptr;
+  const uint32_t *long_mask = nullptr;
+  const int32_t *long_row = nullptr, *long_cs = nullptr;
+};
 
 // Device-side tables the host planner builds once per shard (all optional).
 struct DevPlan {
@@ -82,6 +104,7 @@ struct DevPlan {
   const int32_t *slab_rp = nullptr;
   const int32_t *slab_col = nullptr;
   const void *slab_val = nullptr;
+  DevCsort cs;  // kCsort
 };
 
 struct LaunchPlan {
@@ -110,6 +133,9 @@ hipError_t launch_rows_f32(const DevCSR &A, const DevPlan &dp, const LaunchPlan 
                            const float *x, float *y, hipStream_t st);
 hipError_t launch_rows_f64(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p,
                            const double *x, double *y, hipStream_t st);
+
+// Column-sorted row-block kernel + its finishing pass (csort.hip).
+hipError_t launch_csort(const DevCsort &c, int dtype, const void *x, void *y, hipStream_t st);
 
 // Enqueues one y = A*x (main kernel + split-row kernels when present).
 hipError_t launch_spmv(const DevCSR &A, const DevPlan &dp, int dtype, const LaunchPlan &plan,

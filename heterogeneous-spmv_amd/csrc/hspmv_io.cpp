@@ -590,6 +590,36 @@ int hspmv_build_csr3_maps(const hspmv_csr *A, int ssrs, int srs, hspmv_csr3_buf 
   return HSPMV_OK;
 }
 
+// CSR-2 (spmv-csrk/spmv.cpp:28 CSRK_LEVEL 2): one grouping level with the
+// threshold super_row_size * NNZ / N (csrk.cu:1089-1091), and an identity
+// outer level so the CSR-3 kernels and partitioner take it as it is.
+int hspmv_build_csr2_maps(const hspmv_csr *A, int srs, hspmv_csr3_buf *out) {
+  clear_error();
+  if (!out) return set_error(HSPMV_E_INVALID, "NULL output");
+  memset(out, 0, sizeof(*out));
+  int rc = validate_host_csr(A, true);
+  if (rc) return rc;
+  if (srs < 1) return set_error(HSPMV_E_INVALID, "super_row_size must be >= 1");
+  const int64_t m = A->m, nnz = A->nnz;
+  std::vector<int64_t> deg((size_t)m);
+  for (int64_t i = 0; i < m; ++i) deg[i] = A->row_ptr[i + 1] - A->row_ptr[i];
+  const int64_t thr1 = (int64_t)(int)((int64_t)srs * nnz / (m ? m : 1));
+  std::vector<int32_t> inner;
+  const int64_t n1 = group_by_threshold(m, deg, thr1, &inner);
+  if (n1 == 0) inner.assign(1, 0);
+  out->n_ssr = n1;
+  out->n_sr = n1;
+  out->outer = (int32_t *)malloc(4 * (size_t)(n1 + 1));
+  out->inner = (int32_t *)malloc(4 * (size_t)(n1 + 1));
+  if (!out->outer || !out->inner) {
+    hspmv_free_csr3(out);
+    return set_error(HSPMV_E_NOMEM, "out of host memory");
+  }
+  for (int64_t i = 0; i <= n1; ++i) out->outer[i] = (int32_t)i;
+  memcpy(out->inner, inner.data(), 4 * (size_t)(n1 + 1));
+  return HSPMV_OK;
+}
+
 int hspmv_csr3_params(double d, int flavour, int *ssrs_out, int *srs_out) {
   clear_error();
   if (!ssrs_out || !srs_out || !(d > 0.0)) return set_error(HSPMV_E_INVALID, "bad arguments");

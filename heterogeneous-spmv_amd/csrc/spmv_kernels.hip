@@ -180,6 +180,8 @@ hipError_t launch_typed(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p,
       }
       if (e != hipSuccess) return e;
       break;
+    case kCsort:
+      return launch_csort(dp.cs, sizeof(T) == 8 ? 1 : 0, x, y, st);
     default:
       return hipErrorInvalidValue;
   }
@@ -259,12 +261,18 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   else
     full = footprint <= 192.0 * 1024 * 1024;
   if (k == kAuto)
-    p.kernel = (A.n_ssr > 0) ? kCsr3 : kStream;
+    p.kernel = A.has_csort ? kCsort : ((A.n_ssr > 0) ? kCsr3 : kStream);
   else
     p.kernel = (int)k;
+  if (p.kernel == kCsort && !A.has_csort) p.kernel = (A.n_ssr > 0) ? kCsr3 : kStream;
   if (p.kernel == kCsr3 && A.n_ssr <= 0) p.kernel = kStream;
   const int forced_u = (int)((flags >> 16) & 0x1Fu);  // HSPMV_U(u)
   switch (p.kernel) {
+    case kCsort:  // the workgroup shape is fixed; the host tables hold the rest
+      p.lanes = kWave;
+      p.waves_per_block = kCsortThreads / kWave;
+      p.blocks = 0;  // set from the tables (build_plan_tables)
+      break;
     case kVector: {
       int lanes = (int)((flags >> 4) & 0x7Fu);
       if (lanes == 0) lanes = floor_pow2(d_all < 2.0 ? 2.0 : d_all);
@@ -319,9 +327,9 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
       break;
     }
   }
-  if (p.kernel == kVector) {
+  if (p.kernel == kVector || p.kernel == kCsort) {
     full = false;
-    chunk = 1;  // the vector kernel keeps dispatch order
+    chunk = 1;  // dispatch order (csort: the column parts alternate XCDs)
   }
   if (full) {
     const int64_t per_xcd = p.blocks / 8;

@@ -17,7 +17,7 @@ HEADER = REPO_ROOT / "include" / "hspmv.h"
 
 F32, F64 = 0, 1
 
-KERNEL_AUTO, KERNEL_VECTOR, KERNEL_STREAM, KERNEL_CSR3 = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_VECTOR, KERNEL_STREAM, KERNEL_CSR3, KERNEL_CSORT = 0, 1, 2, 3, 4
 LANES_SHIFT = 4
 FLAG_NO_COL16 = 1 << 11
 FLAG_NONTEMPORAL = 1 << 12
@@ -112,7 +112,7 @@ class Info(C.Structure):
                 ("x_entries", C.c_int64), ("format_bytes", C.c_double), ("col16", C.c_int32),
                 ("wave_tasks", C.c_int32), ("x_windows", C.c_int32), ("x_dict", C.c_int32),
                 ("x_dict_entries", C.c_int64), ("x_slabs", C.c_int32),
-                ("col16_group", C.c_int32)]
+                ("col16_group", C.c_int32), ("csort_parts", C.c_int32)]
 
 
 _P = C.c_void_p
@@ -144,6 +144,9 @@ SIGNATURES = {
     "hspmv_free_csr3": (None, [C.POINTER(Csr3Buf)]),
     "hspmv_build_csr3_maps": (C.c_int, [C.POINTER(Csr), C.c_int, C.c_int, C.POINTER(Csr3Buf)]),
     "hspmv_build_csr3_bandk": (C.c_int, [C.POINTER(Csr), C.c_int, C.c_int, C.POINTER(CsrBuf),
+                                         C.POINTER(Csr3Buf), _P]),
+    "hspmv_build_csr2_maps": (C.c_int, [C.POINTER(Csr), C.c_int, C.POINTER(Csr3Buf)]),
+    "hspmv_build_csr2_bandk": (C.c_int, [C.POINTER(Csr), C.c_int, C.POINTER(CsrBuf),
                                          C.POINTER(Csr3Buf), _P]),
     "hspmv_csr3_params": (C.c_int, [C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hspmv_partition_rows": (C.c_int, [C.c_int64, _P, C.POINTER(Csr3Maps), C.c_int, _P]),

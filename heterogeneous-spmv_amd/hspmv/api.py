@@ -22,12 +22,12 @@ from typing import Optional
 import numpy as np
 
 from . import _lib
-from ._lib import (F32, F64, KERNEL_AUTO, KERNEL_CSR3, KERNEL_STREAM, KERNEL_VECTOR,
+from ._lib import (F32, F64, KERNEL_AUTO, KERNEL_CSORT, KERNEL_CSR3, KERNEL_STREAM, KERNEL_VECTOR,
                    FLAG_DEVICE_PTRS, FLAG_NONTEMPORAL, HspmvError, check, lanes_flag, lib,
                    remap_flag)
 
 _KERNELS = {"auto": KERNEL_AUTO, "vector": KERNEL_VECTOR, "stream": KERNEL_STREAM,
-            "csr3": KERNEL_CSR3}
+            "csr3": KERNEL_CSR3, "csort": KERNEL_CSORT}
 KERNEL_NAMES = {v: k for k, v in _KERNELS.items()}
 
 
@@ -209,6 +209,31 @@ def build_csr3_bandk(A: CsrMatrix, ssrs: int, srs: int):
     return Ap, maps, perm
 
 
+def build_csr2_maps(A: CsrMatrix, super_row_size: int) -> Csr3Maps:
+    """CSR-2 maps (one level; outer = identity): hspmv_build_csr2_maps."""
+    cs, mbuf = A.c_struct(), _lib.Csr3Buf()
+    check(lib().hspmv_build_csr2_maps(C.byref(cs), int(super_row_size), C.byref(mbuf)),
+          "build_csr2_maps")
+    maps = _take_maps(mbuf)
+    if maps is None:
+        maps = Csr3Maps(np.zeros(1, np.int32), np.zeros(1, np.int32))
+    return maps
+
+
+def build_csr2_bandk(A: CsrMatrix, super_row_size: int):
+    """The k = 2 band-k build (hspmv_build_csr2_bandk): (A_perm, maps, perm)
+    as build_csr3_bandk, maps with one super-row per super-super-row."""
+    cs, buf, mbuf = A.c_struct(), _lib.CsrBuf(), _lib.Csr3Buf()
+    perm = np.empty(A.m, np.int32)
+    check(lib().hspmv_build_csr2_bandk(C.byref(cs), int(super_row_size), C.byref(buf),
+                                       C.byref(mbuf), _ptr(perm)), "build_csr2_bandk")
+    Ap = _take_csr(buf)
+    maps = _take_maps(mbuf)
+    if maps is None:
+        maps = Csr3Maps(np.zeros(1, np.int32), np.zeros(1, np.int32))
+    return Ap, maps, perm
+
+
 _FLAVOURS = {"volta": 0, "csr3-writer": 0, "mi100": 1, "mi355x": 2}
 
 
@@ -271,7 +296,7 @@ def version() -> str:
 class SpMV:
     """One SpMV operator y = A x on one or more GPUs (a libhspmv handle).
 
-    ``kernel``: "auto" | "stream" | "vector" | "csr3";  ``lanes``: lanes per row
+    ``kernel``: "auto" | "stream" | "vector" | "csr3" | "csort";  ``lanes``: lanes per row
     for "vector" (0 = auto).  ``device``/``stream``: single-device handle on that
     HIP device / hipStream_t (as an int); otherwise ``num_gpus`` GPUs with the
     row-range partition.

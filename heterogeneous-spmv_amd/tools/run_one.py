@@ -9,6 +9,8 @@ import json
 import sys
 from pathlib import Path
 
+import numpy as np
+
 HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE.parent))
 sys.path.insert(0, str(HERE))
@@ -29,6 +31,8 @@ def main():
     ap.add_argument("--noxcd", action="store_true")
     ap.add_argument("--mi355x-maps", action="store_true")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--cold", type=int, default=0,
+                    help="also time N launches each after a 512 MiB read (Infinity Cache evicted)")
     a = ap.parse_args()
     A, maps, desc = build(a.config)
     if a.kernel == "csr3" and (maps is None or a.mi355x_maps):
@@ -40,9 +44,23 @@ def main():
     op.set_x(gen.rand_x(A.n, 42).astype(A.val.dtype))
     t = op.run(warmup=3, iters=a.iters)
     b = op.info["alg_bytes"]  # x counted as the distinct columns read
-    print(json.dumps({"config": a.config, "desc": desc, "info": op.info, "t_min_us": t["t_min"] * 1e6,
-                      "t_avg_us": t["t_avg"] * 1e6, "alg_bytes": b,
-                      "gbps_min": b / t["t_min"] * 1e-9}))
+    out = {"config": a.config, "desc": desc, "info": op.info, "t_min_us": t["t_min"] * 1e6,
+           "t_avg_us": t["t_avg"] * 1e6, "alg_bytes": b, "gbps_min": b / t["t_min"] * 1e-9,
+           "gbps_avg": b / t["t_avg"] * 1e-9}
+    if a.cold:
+        # cold: a 512 MiB read before every launch evicts the 256 MiB
+        # Infinity Cache; each launch timed alone by the library's events
+        import torch
+        flush = torch.ones(64 << 20, dtype=torch.float64, device="cuda")
+        cold = []
+        for _ in range(a.cold):
+            flush.sum()
+            torch.cuda.synchronize()
+            cold.append(op.run(warmup=0, iters=1)["t_min"])
+        del flush
+        med = float(np.median(cold))
+        out.update({"cold_us": med * 1e6, "cold_min_us": min(cold) * 1e6, "gbps_cold": b / med * 1e-9})
+    print(json.dumps(out))
     op.close()
 
 

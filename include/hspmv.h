@@ -137,6 +137,8 @@ typedef struct {
                           base per 64-row STREAM group or packed CSR3 task
                           (every one spans < 65536 columns); 0 = per
                           256-nonzero blocks or none                        */
+  int32_t csort_parts; /* CSORT: column parts H of the row blocks (0 = the
+                          handle does not use the column-sorted kernel)     */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
@@ -149,6 +151,12 @@ typedef struct hspmv_handle hspmv_handle;
 #define HSPMV_KERNEL_CSR3 3u   /* super-rows packed into <= 64-row wave
                                   tasks, 4 per workgroup (or one workgroup
                                   per super-super-row: HSPMV_CSR3_PLAN=ssr) */
+#define HSPMV_KERNEL_CSORT 4u  /* column-sorted row blocks: each workgroup
+                                  walks its rows' nonzeros in column order,
+                                  fp64 LDS row sums (irregular gathers; not
+                                  bitwise vs omp_spmv: see csort.hip). AUTO
+                                  picks it for HBM-resident matrices whose
+                                  gathers are irregular                      */
 #define HSPMV_KERNEL_MASK 0xFu
 /* lanes per row for VECTOR: HSPMV_LANES(L), L in {1,2,4,8,16,32,64}; 0=auto */
 #define HSPMV_LANES_SHIFT 4
@@ -277,6 +285,17 @@ int hspmv_build_csr3_maps(const hspmv_csr *A, int ssrs, int srs,
  * perm[i] of A (so y = P^T y_out, x_out[i] = x[perm[i]]).  A must be square.
  * Replaces what reformat-csr-to-csr3 (spmv-auto.cpp:183-195) writes. */
 int hspmv_build_csr3_bandk(const hspmv_csr *A, int ssrs, int srs, hspmv_csr_buf *A_out,
+                           hspmv_csr3_buf *maps_out, int32_t *perm);
+/* CSR-2 (one map level; spmv-csrk <file> <num_runs> <super_row_size>,
+ * spmv-csrk/spmv.cpp:97-128 with CSRK_LEVEL 2, cuda-spmv-csrk/cuda/spmv.cu:130):
+ * super-rows of super_row_size * NNZ / N nonzeros (handCoarsen rule), each
+ * its own super-super-row (outer = identity), so every CSR-3 consumer takes
+ * it unchanged.  _maps keeps the file order; _bandk also RCM-orders the
+ * super-row graph and permutes A as the k = 2 band-k build does
+ * (csrk.cu:1072-1096: one coarsening + RCM), outputs as
+ * hspmv_build_csr3_bandk. */
+int hspmv_build_csr2_maps(const hspmv_csr *A, int super_row_size, hspmv_csr3_buf *out);
+int hspmv_build_csr2_bandk(const hspmv_csr *A, int super_row_size, hspmv_csr_buf *A_out,
                            hspmv_csr3_buf *maps_out, int32_t *perm);
 /* Auto parameters.  flavour 0: the .csr3 writer / Volta formula
  * (reformat-csr-to-csr3/spmv-auto.cpp:154-173); 1: the MI100 driver formula

@@ -91,3 +91,44 @@ def test_rejects_rectangular():
                         np.ones(2))
     with pytest.raises(hspmv.HspmvError):
         hspmv.build_csr3_bandk(A, 2, 2)
+
+
+def check_bandk2(A, srs):
+    """CSR-2 (k = 2): one coarsening + RCM (csrk.cu:1072-1096 with k = 2)."""
+    Ap, maps, perm = hspmv.build_csr2_bandk(A, srs)
+    m = A.m
+    assert np.array_equal(np.sort(perm), np.arange(m))
+    assert (abs(_csr(A)[perm][:, perm] - _csr(Ap))).nnz == 0
+    o, i = maps.outer, maps.inner
+    assert maps.n_ssr == maps.n_sr and np.array_equal(o, np.arange(maps.n_sr + 1))
+    assert i[0] == 0 and i[-1] == m and np.all(np.diff(i) > 0)
+    fo = hspmv.build_csr2_maps(A, srs)
+    assert fo.n_sr == maps.n_sr
+    assert np.array_equal(np.sort(np.diff(fo.inner)), np.sort(np.diff(i)))
+    # the super-rows are whole groups of the file order, moved as blocks
+    for s in range(0, maps.n_sr, max(1, maps.n_sr // 200)):
+        rows = perm[i[s]:i[s + 1]]
+        assert np.all(np.diff(rows) == 1)
+    x = gen.rand_x(A.n, 5)
+    y = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    yp = oracle.spmv(Ap.row_ptr, Ap.col_idx, Ap.val, x[perm])
+    assert np.allclose(yp, y[perm], rtol=1e-12, atol=1e-12)
+    return Ap, maps, perm
+
+
+@pytest.mark.parametrize("name,srs", [("lap32.mtx.rcm", 8), ("powerlaw1500", 10),
+                                      ("banded3000", 4), ("empty_rows", 2)])
+def test_csr2_invariants_on_fixtures(name, srs):
+    A = hspmv.read_csr(GOLDEN / f"{name}.csr", np.float64)
+    check_bandk2(A, srs)
+
+
+def test_csr2_on_generators_and_shuffled_order_is_recovered():
+    check_bandk2(gen.stencil27(14), 10)
+    # a shuffled Laplacian: the RCM of the super-row graph brings the band back
+    A = _shuffled(gen.laplace2d(40, 40), 11)
+    Ap, maps, perm = check_bandk2(A, 1)
+    rows = np.repeat(np.arange(Ap.m), np.diff(Ap.row_ptr))
+    bw = np.abs(Ap.col_idx - rows).max()
+    rows0 = np.repeat(np.arange(A.m), np.diff(A.row_ptr))
+    assert bw < np.abs(A.col_idx - rows0).max() / 4

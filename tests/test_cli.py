@@ -124,3 +124,51 @@ def test_spmv_csrk_bandk_reorders_and_restores_file_order(tmp_path):
         assert "Check: PASS" in p.stdout and "reordered in" in p.stdout
         y = np.fromfile(out, np.float64)
         assert np.all(np.abs(y - y_ref) <= 1e-6 * np.abs(y_ref) + 1e-12 * absrow)
+
+
+def harness_value(out: str, key: str) -> float:
+    i = out.find(key)
+    j = out.find("\n", i)
+    return float(out[i + len(key):j])
+
+
+@pytest.mark.gpu
+def test_spmv_csrk_csr2_three_argument_form(tmp_path):
+    # spmv-csrk <file> <num_runs> <super_row_size>: CSR-2, one map level
+    # (spmv-csrk/spmv.cpp:97-128, CSRK_LEVEL 2); band-k (default) and file
+    # order, y back in file order checked against the oracle
+    import hspmv
+    A = hspmv.read_csr(GOLDEN / "powerlaw1500.csr", np.float64)
+    x = gen.rand_x(A.n, 5)
+    y_ref = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    for extra in ([], ["--file-order"]):
+        out = tmp_path / "y.bin"
+        p = run(BUILD / "spmv-csrk", GOLDEN / "powerlaw1500.csr", 5, 8, "--x", "rand:5",
+                "--dump-y", out, *extra)
+        assert "SpMV\nHAND\n2\n8\n" in p.stdout, p.stdout
+        assert "Check: PASS" in p.stdout and "Number Wrong: 0" in p.stdout
+        m = re.search(r"super-super-rows (\d+) super-rows (\d+)", p.stdout)
+        assert m and m.group(1) == m.group(2)  # one super-row per super-super-row
+        y = np.fromfile(out, np.float64)
+        assert np.all(np.abs(y - y_ref) <= 1e-6 * np.abs(y_ref) + 1e-12 * absrow)
+        harness_parse(p.stdout)
+    # a bad size fails loudly
+    p = run(BUILD / "spmv-csrk", GOLDEN / "powerlaw1500.csr", 5, 0, check=False)
+    assert p.returncode != 0
+
+
+@pytest.mark.gpu
+def test_cli_gflops_printed_from_timemin():
+    # GFLOPs / GBps are computed from TimeMin (what run_norm.py records), the
+    # event-timed rates are KernelGFLOPs / KernelGBps
+    import hspmv
+    A = hspmv.read_csr(GOLDEN / "lap32.mtx.rcm.csr", np.float64)
+    p = run(BUILD / "spmv-csr", GOLDEN / "lap32.mtx.rcm.csr", 9)
+    tmin = harness_value(p.stdout, "TimeMin:")
+    g = harness_value(p.stdout, "GFLOPs:")
+    assert abs(g - 2.0 * A.nnz / tmin * 1e-9) <= 1e-5 * g
+    kmin = harness_value(p.stdout, "KernelMin:")
+    kg = harness_value(p.stdout, "KernelGFLOPs:")
+    assert abs(kg - 2.0 * A.nnz / kmin * 1e-9) <= 1e-5 * kg
+    assert "KernelGBps:" in p.stdout and "GBps:" in p.stdout

@@ -1,0 +1,186 @@
+"""The column-sorted row-block kernel (HSPMV_KERNEL_CSORT, csrc/csort.hip)
+against the oracle.
+
+csort walks each row block's nonzeros in column order and adds the products
+into fp64 LDS row slots with atomics, so its y is NOT omp_spmv's left-to-right
+sum bit for bit.  What is checked instead, on the same seeded inputs:
+
+* fp64 data: within the north-star bar |y - y64| <= 1e-6 |y64| + 1e-12 sum|a x|
+  (the products are omp_spmv's; only the order of the fp64 additions differs);
+* fp32 data: y is the fp32 rounding of the fp64 sum of the exact products, so
+  within half an fp32 ulp (+ the fp64 summation error) of the exact sum, and
+  within omp_spmv's own fp32 summation error of the reference's y;
+* repeatability, long rows cut into slices (first/last/adjacent rows, and with
+  HSPMV_FLAG_NO_SPLIT kept whole), empty rows and blocks, 1/2/4 column parts,
+  chunk sizes, an Inf in x (padding must not spread it), and the planner's
+  auto choice (irregular gathers only).
+"""
+import numpy as np
+import pytest
+
+import hspmv
+import oracle
+from conftest import GOLDEN, fp64_tol_ok
+from hspmv import gen
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    assert hspmv.device_count() >= 1, "no HIP device visible: run on the MI355X box"
+
+
+def run(A, x, maps=None, **kw):
+    with hspmv.SpMV(A, maps, **kw) as op:
+        return op(x), op.info
+
+
+def exact64(A, x):
+    return oracle.spmv(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
+
+
+def check(A, x, y):
+    y64 = exact64(A, x)
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    if A.val.dtype == np.float64:
+        assert fp64_tol_ok(y, y64, absrow), np.abs(y - y64).max()
+    else:
+        err = np.abs(y.astype(np.float64) - y64)
+        assert np.all(err <= 2.0 ** -24 * np.abs(y64) + 1e-12 * absrow), err.max()
+        y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+        lens = np.diff(A.row_ptr)
+        e32 = np.abs(y.astype(np.float64) - y32.astype(np.float64))
+        assert np.all(e32 <= (lens + 2) * 2.0 ** -23 * absrow + 1e-30)
+    return y64
+
+
+def _long_rows(seed=3, m=900, n=200_000):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 30, m)
+    lens[rng.integers(0, m, 30)] = rng.integers(33, 4000, 30)
+    for r, ln in [(0, 90_000), (1, 4097), (63, 5000), (64, 9000), (65, 4096), (400, 30_000),
+                  (401, 60_000), (m - 1, 8193)]:
+        lens[r] = ln
+    rp = np.concatenate([[0], np.cumsum(lens)])
+    ci = np.concatenate([np.sort(rng.choice(n, ln, replace=False)) for ln in lens])
+    return hspmv.CsrMatrix(m, n, rp, ci, rng.uniform(-1, 1, rp[-1]))
+
+
+def _matrices():
+    yield "powerlaw1500", hspmv.read_csr(GOLDEN / "powerlaw1500.csr", np.float64)
+    yield "long_row", hspmv.read_csr(GOLDEN / "long_row.csr", np.float64)
+    yield "empty_rows", hspmv.read_csr(GOLDEN / "empty_rows.csr", np.float64)
+    yield "single_row", hspmv.read_csr(GOLDEN / "single_row.csr", np.float64)
+    yield "lap32", hspmv.read_csr(GOLDEN / "lap32.mtx.rcm.csr", np.float64)
+    yield "powerlaw60k", gen.powerlaw(60_000, seed=5, dtype=np.float64)
+    yield "long_rows", _long_rows()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("parts", ["1", "2", "4"])
+def test_csort_matches_oracle(dtype, parts, monkeypatch):
+    monkeypatch.setenv("HSPMV_CSORT_H", parts)
+    for name, A in _matrices():
+        A = A.astype(dtype)
+        x = gen.rand_x(A.n, 17).astype(dtype)
+        y, info = run(A, x, kernel="csort")
+        assert info["kernel_name"] == "csort", name
+        assert info["csort_parts"] == min(int(parts), A.n), name
+        assert info["n_split_rows"] == int((np.diff(A.row_ptr) > 4096).sum()), name
+        check(A, x, y)
+
+
+@pytest.mark.parametrize("u", ["4", "8", "16"])
+def test_csort_chunk_sizes_and_nontemporal(u, monkeypatch):
+    monkeypatch.setenv("HSPMV_CSORT_U", u)
+    A = gen.powerlaw(50_000, seed=9, dtype=np.float32)
+    x = gen.rand_x(A.n, 3).astype(np.float32)
+    for nt in ("0", "1"):
+        monkeypatch.setenv("HSPMV_CSORT_NT", nt)
+        y, info = run(A, x, kernel="csort")
+        assert info["chunk_u"] == int(u)
+        check(A, x, y)
+
+
+def test_csort_long_rows_whole_and_sliced():
+    A = _long_rows(seed=8)
+    x = gen.rand_x(A.n, 2)
+    lens = np.diff(A.row_ptr)
+    y1, i1 = run(A, x, kernel="csort")
+    assert i1["n_split_rows"] == int((lens > 4096).sum())
+    check(A, x, y1)
+    y2, i2 = run(A, x, kernel="csort", split_rows=False)  # long rows stay one slot
+    assert i2["n_split_rows"] == 0
+    check(A, x, y2)
+
+
+def test_csort_repeatable_fp32():
+    A = gen.powerlaw(200_000, seed=4, dtype=np.float32)
+    x = gen.rand_x(A.n, 8).astype(np.float32)
+    with hspmv.SpMV(A, kernel="csort") as op:
+        ys = [op(x) for _ in range(4)]
+    # fp64 sums rounded once: equal run to run except where an fp64 sum sits
+    # within its own rounding of an fp32 tie
+    for y in ys[1:]:
+        assert np.mean(ys[0] == y) > 0.9999
+    check(A, x, ys[0])
+
+
+def test_csort_padding_does_not_spread_inf():
+    A = gen.powerlaw(30_000, seed=6, dtype=np.float64)
+    x = gen.rand_x(A.n, 5)
+    c = int(A.col_idx[A.row_ptr[100]])
+    x[c] = np.inf
+    y, _ = run(A, x, kernel="csort")
+    touched = np.zeros(A.m, bool)
+    rows = np.repeat(np.arange(A.m), np.diff(A.row_ptr))
+    touched[rows[A.col_idx == c]] = True
+    assert not np.any(np.isnan(y[~touched])) and np.all(np.isfinite(y[~touched]))
+    xs = x.copy()
+    xs[c] = 0.0
+    ys = exact64(A, xs)
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, xs)
+    assert fp64_tol_ok(y[~touched], ys[~touched], absrow[~touched])
+
+
+def test_csort_empty_and_degenerate():
+    # all-empty rows, one column, more row blocks than rows
+    for m, n, lens in [(500, 1, np.ones(500, int)), (3, 7, np.array([0, 7, 0])),
+                       (2000, 3000, np.zeros(2000, int))]:
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        ci = np.concatenate([np.arange(ln) % n for ln in lens]).astype(np.int32) if rp[-1] else \
+            np.zeros(0, np.int32)
+        A = hspmv.CsrMatrix(m, n, rp, ci, np.linspace(-1, 1, rp[-1]))
+        x = gen.rand_x(n, 1)
+        y, info = run(A, x, kernel="csort")
+        check(A, x, y)
+
+
+def test_csort_auto_only_for_irregular_gathers():
+    # banded / stencil matrices keep the ordered row kernels; a small random
+    # matrix (cache-resident) too; csr3 maps do not stop the choice
+    _, i1 = run(gen.banded(200_000, seed=2), gen.rand_x(200_000, 1))
+    assert i1["kernel_name"] == "stream"
+    _, i2 = run(gen.powerlaw(50_000, seed=2, dtype=np.float64), gen.rand_x(50_000, 1))
+    assert i2["kernel_name"] == "stream"
+    A = gen.powerlaw(2_000_000, seed=12, dtype=np.float32)
+    maps = hspmv.build_csr3_maps(A, 64, 4)
+    x = gen.rand_x(A.n, 2).astype(np.float32)
+    y, i3 = run(A, x, maps)
+    assert i3["kernel_name"] == "csort"
+    check(A, x, y)
+    # an explicit row kernel is honoured
+    _, i4 = run(A, x, maps, kernel="csr3")
+    assert i4["kernel_name"] == "csr3"
+
+
+def test_csort_c5_shape_multi_shard():
+    # two row-range shards of a power-law matrix, each its own csort handle,
+    # assemble the full y (the per-rank layout of bench.py / hspmv.dist)
+    A = gen.powerlaw(400_000, seed=7, dtype=np.float32)
+    x = gen.rand_x(A.n, 4).astype(np.float32)
+    splits = hspmv.partition_rows(A.row_ptr, 2)
+    y = np.concatenate([run(A.rows(int(splits[r]), int(splits[r + 1])), x, kernel="csort")[0]
+                        for r in range(2)])
+    check(A, x, y)

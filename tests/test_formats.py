@@ -158,3 +158,17 @@ def test_alg_bytes_formula():
     assert b == 4_996_000 * 12 + 1_000_001 * 4 + 2 * 8_000_000
     assert abs(b / 1e6 - 79.95) < 0.01
     assert hspmv.alg_bytes(10, 10, 30, np.float32, 2, 5) == 30 * 8 + 11 * 4 + 80 + 9 * 4
+
+
+def test_csr2_maps_are_the_first_level_of_the_csr3_grouping():
+    # CSR-2 (one level, spmv-csrk/spmv.cpp:28 CSRK_LEVEL 2): inner = the
+    # oracle's level-1 handCoarsen grouping at threshold srs*NNZ/N, outer = identity
+    for A, srs in [(gen.laplace2d(100, 100), 8), (gen.stencil27(12), 10),
+                   (gen.powerlaw(5000, seed=2, dtype=np.float64), 4),
+                   (hspmv.read_csr(GOLDEN / "empty_rows.csr"), 2)]:
+        maps = hspmv.build_csr2_maps(A, srs)
+        _, inner = oracle.build_maps(A.row_ptr, A.col_idx, srs, 1)
+        assert np.array_equal(maps.inner, inner)
+        assert np.array_equal(maps.outer, np.arange(maps.n_sr + 1))
+    with pytest.raises(hspmv.HspmvError):
+        hspmv.build_csr2_maps(gen.laplace2d(4, 4), 0)
