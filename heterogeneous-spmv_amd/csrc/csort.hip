@@ -52,7 +52,25 @@ __device__ __forceinline__ int32_t wave_uniform(int32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+// Loads chunk c's U entries per lane (idx, value).
 template <typename T, int U, bool NT>
+__device__ __forceinline__ void load_entries(const void *__restrict__ ent, const T *__restrict__ val,
+                                             int32_t c, int lane, uint32_t (&ix)[U], T (&vv)[U]) {
+  const int64_t k0 = (int64_t)c * (kWave * U) + lane;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if constexpr (sizeof(T) == 4) {
+      const u32x2 p = ld<NT>(reinterpret_cast<const u32x2 *>(ent) + k0 + u * kWave);
+      ix[u] = p.x;
+      vv[u] = __uint_as_float(p.y);
+    } else {
+      ix[u] = ld<NT>(reinterpret_cast<const uint32_t *>(ent) + k0 + u * kWave);
+      vv[u] = ld<NT>(val + k0 + u * kWave);
+    }
+  }
+}
+
+template <typename T, int U, bool NT, bool PF>
 __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     int32_t H, int64_t m, int32_t direct, const int32_t *__restrict__ blk_c,
     const int32_t *__restrict__ blk_r, const int32_t *__restrict__ blk_v,
@@ -71,33 +89,38 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   for (int32_t i = threadIdx.x; i <= nr + nv; i += kCsortThreads) acc[i] = 0.0;  // + dummy
   __syncthreads();
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+  uint32_t ix[U];
+  T vv[U];
+  // PF: the next chunk's entries are loaded while this chunk's gathers are
+  // in flight (software pipelining across the wave's chunks)
+  if constexpr (PF)
+    if (c0 + wid < c1) load_entries<T, U, NT>(ent, val, c0 + wid, lane, ix, vv);
   for (int32_t c = c0 + wid; c < c1; c += NW) {  // wave-uniform
     const int32_t base = wave_uniform(cbase[wave_uniform(c)]);
-    const int64_t k0 = (int64_t)c * (kWave * U) + lane;
-    uint32_t ix[U];
-    T vv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if constexpr (sizeof(T) == 4) {
-        const u32x2 p = ld<NT>(reinterpret_cast<const u32x2 *>(ent) + k0 + u * kWave);
-        ix[u] = p.x;
-        vv[u] = __uint_as_float(p.y);
-      } else {
-        ix[u] = ld<NT>(reinterpret_cast<const uint32_t *>(ent) + k0 + u * kWave);
-        vv[u] = ld<NT>(val + k0 + u * kWave);
-      }
-    }
+    if constexpr (!PF) load_entries<T, U, NT>(ent, val, c, lane, ix, vv);
     T xv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) xv[u] = x[base + (int32_t)(ix[u] & 0xffffu)];
+    uint32_t ixc[U];
+    T vvc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ixc[u] = ix[u];
+      vvc[u] = vv[u];
+    }
+    if constexpr (PF) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + NW < c1) load_entries<T, U, NT>(ent, val, c + NW, lane, ix, vv);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       double pr;
       if constexpr (sizeof(T) == 4)
-        pr = (double)vv[u] * (double)xv[u];  // exact
+        pr = (double)vvc[u] * (double)xv[u];  // exact
       else
-        pr = (double)(vv[u] * xv[u]);  // omp_spmv's rounded product
-      atomicAdd(&acc[ix[u] >> 16], pr);
+        pr = (double)(vvc[u] * xv[u]);  // omp_spmv's rounded product
+      atomicAdd(&acc[ixc[u] >> 16], pr);
     }
   }
   __syncthreads();
@@ -139,9 +162,14 @@ __global__ __launch_bounds__(256) void hspmv_csort_finish(
 
 template <typename T, int U, bool NT>
 hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
-  hipLaunchKernelGGL((hspmv_csort<T, U, NT>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
-                     (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
-                     c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, c.part, c.spart, y);
+  if (c.prefetch)
+    hipLaunchKernelGGL((hspmv_csort<T, U, NT, true>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
+                       (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
+                       c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, c.part, c.spart, y);
+  else
+    hipLaunchKernelGGL((hspmv_csort<T, U, NT, false>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
+                       (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
+                       c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, c.part, c.spart, y);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || c.direct) return e;
   const int64_t rb = (c.m + 255) / 256;

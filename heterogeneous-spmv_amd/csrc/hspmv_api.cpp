@@ -110,6 +110,7 @@ struct hspmv_handle {
   bool x_set = false;
   bool borrowed = false;  // HSPMV_FLAG_DEVICE_PTRS: matrix arrays not owned
   int64_t max_rows = 0;   // multi-GPU padding for the y all-gather
+  bool sharded = false;   // row-range partition (hspmv_create_sharded / num_gpus > 1)
   int64_t x_entries() const {
     int64_t t = 0;
     for (auto &s : shards) t += s.x_entries;
@@ -1020,6 +1021,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.n_long = (int32_t)lrow.size();
   c.nontemporal = true;  // the entry stream is read once; keep x in the caches
   if (const char *e = getenv("HSPMV_CSORT_NT")) c.nontemporal = atoi(e) != 0;
+  if (const char *e = getenv("HSPMV_CSORT_PF")) c.prefetch = atoi(e) != 0;
   c.m = m;
   c.lds_bytes = 8 * max_slots;
   c.blk_c = s.d_cs_blk_c;
@@ -1423,13 +1425,19 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
     // the values come back to the host too: the x slabs copy them slab-major
     std::vector<char> vals(dtype_size(A->dtype) * (size_t)A->nnz);
     if (A->nnz) HIP_TRY(hipMemcpy(vals.data(), A->val, vals.size(), hipMemcpyDeviceToHost));
-    if ((rc = build_row_tables(s, rp.data(), cols.data(), vals.data(), A->m, A->n, A->dtype, flags)))
+    // from here on the shard owns device memory: every error path frees it
+    if ((rc = build_row_tables(s, rp.data(), cols.data(), vals.data(), A->m, A->n, A->dtype, flags))) {
+      free_shard(s, true);
       return rc;
+    }
     std::vector<char>().swap(vals);
     std::vector<int32_t>().swap(cols);
     const size_t sv = dtype_size(A->dtype);
-    if ((rc = dev_alloc(&s.d_x, sv * (size_t)A->n, &s.bytes))) return rc;
-    if ((rc = dev_alloc(&s.d_y, sv * (size_t)A->m, &s.bytes))) return rc;
+    if ((rc = dev_alloc(&s.d_x, sv * (size_t)A->n, &s.bytes)) ||
+        (rc = dev_alloc(&s.d_y, sv * (size_t)A->m, &s.bytes))) {
+      free_shard(s, true);
+      return rc;
+    }
   }
   if ((rc = finish_shard(s, A->dtype, flags, stream))) {
     free_shard(s, h->borrowed);
@@ -1439,20 +1447,19 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
   return HSPMV_OK;
 }
 
-int hspmv_create(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps, int num_gpus,
-                 unsigned flags) {
-  clear_error();
-  if (!hp) return set_error(HSPMV_E_INVALID, "NULL handle pointer");
-  *hp = nullptr;
-  if (flags & HSPMV_FLAG_DEVICE_PTRS)
-    return set_error(HSPMV_E_INVALID, "device pointers need hspmv_create_on_device");
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
-    return set_error(HSPMV_E_NODEV, "no HIP device available");
-  if (num_gpus <= 0) num_gpus = ndev;
-  if (num_gpus > ndev)
-    return set_error(HSPMV_E_NODEV, "%d GPUs requested, %d visible", num_gpus, ndev);
-  if (num_gpus == 1) return hspmv_create_on_device(hp, A, maps, 0, nullptr, flags);
+}  // extern "C"
+
+namespace {
+
+// The row-range partition over the devices devs[0..P) (one shard each; a
+// device may appear more than once).  Distinct devices exchange x and y with
+// RCCL (one communicator per shard, ncclCommInitAll); a list that repeats a
+// device exchanges by device-to-device copies instead (RCCL allows one rank
+// per device), which is how the partition, the padded y all-gather and the
+// unpadding are exercised on a one-GPU box.
+int create_sharded(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps,
+                   const std::vector<int> &devs, unsigned flags) {
+  const int num_gpus = (int)devs.size();
   int rc;
   if ((rc = validate_host_csr(A, true))) return rc;
   if ((rc = validate_host_maps(maps, A->m))) return rc;
@@ -1483,7 +1490,7 @@ int hspmv_create(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *m
   };
   for (int p = 0; p < num_gpus; ++p) {
     Shard &s = h->shards[p];
-    s.device = p;
+    s.device = devs[(size_t)p];
     if ((rc = upload_shard(s, A, maps, splits[p], splits[p + 1], ssr_split[p], ssr_split[p + 1], 0,
                            flags))) {
       cleanup();
@@ -1500,21 +1507,119 @@ int hspmv_create(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *m
       return rc;
     }
   }
-  h->comms.resize((size_t)num_gpus);
-  std::vector<int> devs((size_t)num_gpus);
-  for (int p = 0; p < num_gpus; ++p) devs[p] = p;
-  ncclResult_t r = ncclCommInitAll(h->comms.data(), num_gpus, devs.data());
-  if (r != ncclSuccess) {
-    cleanup();
-    h->comms.clear();
-    return set_error(HSPMV_E_RCCL, "ncclCommInitAll: %s", ncclGetErrorString(r));
+  std::vector<int> sorted(devs);
+  std::sort(sorted.begin(), sorted.end());
+  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  if (distinct) {
+    h->comms.resize((size_t)num_gpus);
+    std::vector<int> dl(devs);
+    ncclResult_t r = ncclCommInitAll(h->comms.data(), num_gpus, dl.data());
+    if (r != ncclSuccess) {
+      cleanup();
+      h->comms.clear();
+      return set_error(HSPMV_E_RCCL, "ncclCommInitAll: %s", ncclGetErrorString(r));
+    }
   }
+  h->sharded = true;
   *hp = h.release();
   return HSPMV_OK;
 }
 
+int check_devices(const int *devices, int n, int *ndev_out) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+    return set_error(HSPMV_E_NODEV, "no HIP device available");
+  *ndev_out = ndev;
+  for (int p = 0; devices && p < n; ++p)
+    if (devices[p] < 0 || devices[p] >= ndev)
+      return set_error(HSPMV_E_NODEV, "device %d out of range (have %d)", devices[p], ndev);
+  return HSPMV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hspmv_create(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps, int num_gpus,
+                 unsigned flags) {
+  clear_error();
+  if (!hp) return set_error(HSPMV_E_INVALID, "NULL handle pointer");
+  *hp = nullptr;
+  if (flags & HSPMV_FLAG_DEVICE_PTRS)
+    return set_error(HSPMV_E_INVALID, "device pointers need hspmv_create_on_device");
+  int ndev = 0, rc;
+  if ((rc = check_devices(nullptr, 0, &ndev))) return rc;
+  if (num_gpus <= 0) num_gpus = ndev;
+  if (num_gpus > ndev)
+    return set_error(HSPMV_E_NODEV, "%d GPUs requested, %d visible", num_gpus, ndev);
+  if (num_gpus == 1) return hspmv_create_on_device(hp, A, maps, 0, nullptr, flags);
+  std::vector<int> devs((size_t)num_gpus);
+  for (int p = 0; p < num_gpus; ++p) devs[(size_t)p] = p;
+  return create_sharded(hp, A, maps, devs, flags);
+}
+
+int hspmv_create_sharded(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps,
+                         const int *devices, int n_shards, unsigned flags) {
+  clear_error();
+  if (!hp) return set_error(HSPMV_E_INVALID, "NULL handle pointer");
+  *hp = nullptr;
+  if (flags & HSPMV_FLAG_DEVICE_PTRS)
+    return set_error(HSPMV_E_INVALID, "device pointers need hspmv_create_on_device");
+  if (!devices || n_shards < 1) return set_error(HSPMV_E_INVALID, "need n_shards >= 1 devices");
+  int ndev = 0, rc;
+  if ((rc = check_devices(devices, n_shards, &ndev))) return rc;
+  return create_sharded(hp, A, maps, std::vector<int>(devices, devices + n_shards), flags);
+}
+
+// Shards that share a device (no communicators): the same exchanges as
+// device-to-device copies on each destination shard's stream, after the
+// source shard's stream has reached them.
+static int copy_exchange(hspmv_handle *h, bool x_bcast) {
+  const size_t sv = dtype_size(h->dtype);
+  const size_t P = h->shards.size();
+  std::vector<hipEvent_t> done(P, nullptr);
+  int rc = HSPMV_OK;
+  for (size_t p = 0; p < P && rc == HSPMV_OK; ++p) {
+    Shard &s = h->shards[p];
+    if (hipSetDevice(s.device) != hipSuccess ||
+        hipEventCreateWithFlags(&done[p], hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(done[p], s.stream) != hipSuccess)
+      rc = set_error(HSPMV_E_HIP, "exchange: event setup on GPU %d failed", s.device);
+  }
+  for (size_t q = 0; q < P && rc == HSPMV_OK; ++q) {
+    Shard &d = h->shards[q];
+    if (hipSetDevice(d.device) != hipSuccess) {
+      rc = set_error(HSPMV_E_HIP, "hipSetDevice(%d) failed", d.device);
+      break;
+    }
+    for (size_t p = 0; p < P && rc == HSPMV_OK; ++p) {
+      const Shard &src = h->shards[x_bcast ? 0 : p];
+      if (x_bcast && q == 0) break;
+      if (hipStreamWaitEvent(d.stream, done[x_bcast ? 0 : p], 0) != hipSuccess) {
+        rc = set_error(HSPMV_E_HIP, "exchange: stream wait failed");
+        break;
+      }
+      hipError_t e;
+      if (x_bcast) {
+        e = hipMemcpyPeerAsync(d.d_x, d.device, src.d_x, src.device, sv * (size_t)h->n, d.stream);
+      } else {
+        char *dst = (char *)d.d_yfull + sv * (size_t)(h->max_rows * (int64_t)p);
+        e = dst == src.d_y ? hipSuccess
+                           : hipMemcpyPeerAsync(dst, d.device, src.d_y, src.device,
+                                                sv * (size_t)src.A.m, d.stream);
+      }
+      if (e != hipSuccess) rc = set_error(HSPMV_E_HIP, "exchange copy failed: %s", hipGetErrorString(e));
+      if (x_bcast) break;
+    }
+  }
+  for (size_t p = 0; p < P; ++p)
+    if (done[p]) (void)hipEventDestroy(done[p]);
+  return rc;
+}
+
 static int bcast_x(hspmv_handle *h) {
-  if (h->shards.size() < 2) return HSPMV_OK;
+  if (!h->sharded) return HSPMV_OK;
+  if (h->comms.empty()) return copy_exchange(h, true);
   const ncclDataType_t dt = h->dtype == HSPMV_F64 ? ncclFloat64 : ncclFloat32;
   RCCL_TRY(ncclGroupStart());
   for (size_t p = 0; p < h->shards.size(); ++p) {
@@ -1526,7 +1631,8 @@ static int bcast_x(hspmv_handle *h) {
 }
 
 static int gather_y(hspmv_handle *h) {
-  if (h->shards.size() < 2) return HSPMV_OK;
+  if (!h->sharded) return HSPMV_OK;
+  if (h->comms.empty()) return copy_exchange(h, false);
   const ncclDataType_t dt = h->dtype == HSPMV_F64 ? ncclFloat64 : ncclFloat32;
   RCCL_TRY(ncclGroupStart());
   for (size_t p = 0; p < h->shards.size(); ++p) {
@@ -1563,7 +1669,7 @@ int hspmv_bind_x_device(hspmv_handle *h, const void *x_dev) {
   clear_error();
   int rc;
   if ((rc = check_handle(h))) return rc;
-  if (h->shards.size() != 1) return set_error(HSPMV_E_STATE, "bind needs a single-device handle");
+  if (h->sharded) return set_error(HSPMV_E_STATE, "bind needs a single-device handle");
   h->shards[0].x = x_dev ? x_dev : h->shards[0].d_x;
   h->x_set = x_dev != nullptr || h->x_set;
   return HSPMV_OK;
@@ -1573,7 +1679,7 @@ int hspmv_bind_y_device(hspmv_handle *h, void *y_dev) {
   clear_error();
   int rc;
   if ((rc = check_handle(h))) return rc;
-  if (h->shards.size() != 1) return set_error(HSPMV_E_STATE, "bind needs a single-device handle");
+  if (h->sharded) return set_error(HSPMV_E_STATE, "bind needs a single-device handle");
   h->shards[0].y = y_dev ? y_dev : h->shards[0].d_y;
   return HSPMV_OK;
 }
@@ -1660,7 +1766,7 @@ int hspmv_get_y(hspmv_handle *h, void *y_host) {
   if ((rc = check_handle(h))) return rc;
   if (!y_host && h->m > 0) return set_error(HSPMV_E_INVALID, "y is NULL");
   const size_t sv = dtype_size(h->dtype);
-  if (h->shards.size() == 1) {
+  if (!h->sharded) {
     Shard &s = h->shards[0];
     HIP_TRY(hipSetDevice(s.device));
     if (h->m) HIP_TRY(hipMemcpyAsync(y_host, s.y, sv * (size_t)h->m, hipMemcpyDeviceToHost, s.stream));

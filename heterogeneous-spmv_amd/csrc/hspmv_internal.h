@@ -56,6 +56,7 @@ constexpr int kCsortMaxLds = 160 * 1024;
 struct DevCsort {
   int32_t n_wg = 0, H = 1, u = 16, direct = 0, n_long = 0;
   bool nontemporal = true;
+  bool prefetch = false;  // next chunk's entries loaded during this chunk's gathers
   int64_t m = 0;
   int32_t lds_bytes = 0;
   const int32_t *blk_c = nullptr, *blk_r = nullptr, *blk_v = nullptr, *vslice = nullptr;

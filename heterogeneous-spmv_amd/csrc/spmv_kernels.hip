@@ -327,6 +327,23 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
       break;
     }
   }
+  // The STREAM / CSR3 kernels address x and the matrix streams as a 64-bit
+  // base plus a 32-bit byte offset (spmv_device.cuh ld_off): x of 4 GiB or
+  // more (fp64: n >= 2^29), or -- without split rows -- a row group that
+  // could stream 4 GiB, would wrap.  Such matrices take a kernel that
+  // indexes through pointers: csort when it was built, else VECTOR.
+  const double max_run_bytes =
+      (flags & (1u << 15)) ? (double)A.nnz * (sv > 4.0 ? sv : 4.0) : 64.0 * kLongRow * sv;
+  if ((p.kernel == kStream || p.kernel == kCsr3) &&
+      ((double)A.n * sv > 4294967295.0 || max_run_bytes > 4294967295.0))
+    p.kernel = A.has_csort ? kCsort : kVector;
+  if (p.kernel == kVector && !(k == kVector)) {  // re-plan the vector launch shape
+    p.lanes = floor_pow2(d_all < 2.0 ? 2.0 : d_all);
+    const int64_t threads = (int64_t)A.m * p.lanes;
+    const int64_t cap = 256LL * 8 * 16;
+    p.blocks = (threads + 255) / 256 < cap ? (threads + 255) / 256 : cap;
+    if (p.blocks < 1) p.blocks = 1;
+  }
   if (p.kernel == kVector || p.kernel == kCsort) {
     full = false;
     chunk = 1;  // dispatch order (csort: the column parts alternate XCDs)

@@ -122,6 +122,8 @@ SIGNATURES = {
     "hspmv_create": (C.c_int, [C.POINTER(_H), C.POINTER(Csr), C.POINTER(Csr3Maps), C.c_int, C.c_uint]),
     "hspmv_create_on_device": (C.c_int, [C.POINTER(_H), C.POINTER(Csr), C.POINTER(Csr3Maps),
                                          C.c_int, _P, C.c_uint]),
+    "hspmv_create_sharded": (C.c_int, [C.POINTER(_H), C.POINTER(Csr), C.POINTER(Csr3Maps),
+                                       C.POINTER(C.c_int), C.c_int, C.c_uint]),
     "hspmv_set_x": (C.c_int, [_H, _P]),
     "hspmv_bind_x_device": (C.c_int, [_H, _P]),
     "hspmv_bind_y_device": (C.c_int, [_H, _P]),

@@ -298,8 +298,9 @@ class SpMV:
 
     ``kernel``: "auto" | "stream" | "vector" | "csr3" | "csort";  ``lanes``: lanes per row
     for "vector" (0 = auto).  ``device``/``stream``: single-device handle on that
-    HIP device / hipStream_t (as an int); otherwise ``num_gpus`` GPUs with the
-    row-range partition.
+    HIP device / hipStream_t (as an int); ``devices``: row-range shards on that
+    device list (hspmv_create_sharded; devices may repeat); otherwise
+    ``num_gpus`` GPUs with the row-range partition.
     """
 
     def __init__(self, A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, num_gpus: int = 1,
@@ -307,7 +308,7 @@ class SpMV:
                  device: Optional[int] = None, stream: Optional[int] = None,
                  xcd_remap: Optional[bool] = None, split_rows: bool = True, chunk_u: int = 0,
                  prefetch: Optional[bool] = None, xcd_chunk: int = 0, groups_per_wave: int = 0,
-                 col16: Optional[bool] = None):
+                 col16: Optional[bool] = None, devices: Optional[list] = None):
         self.A = A
         self.maps = maps
         self.dtype = A.val.dtype
@@ -324,7 +325,12 @@ class SpMV:
         cs = A.c_struct()
         ms = maps.c_struct() if maps is not None else None
         h = C.c_void_p()
-        if device is not None:
+        if devices is not None:  # row-range shards on an explicit device list
+            dl = (C.c_int * len(devices))(*[int(d) for d in devices])
+            rc = lib().hspmv_create_sharded(C.byref(h), C.byref(cs),
+                                            C.byref(ms) if ms is not None else None, dl,
+                                            len(devices), flags)
+        elif device is not None:
             rc = lib().hspmv_create_on_device(C.byref(h), C.byref(cs),
                                               C.byref(ms) if ms is not None else None,
                                               int(device), stream, flags)

@@ -49,12 +49,23 @@ static void fill_x(std::vector<double> &x, unsigned long long seed) {
   }
 }
 
+// Cold-cache flush: READ 512 MiB (one sum per block), so no dirty lines are
+// left whose write-back the next timed launch would pay for.
+__global__ void flush_read(const double *__restrict__ p, size_t n, double *__restrict__ out) {
+  double s = 0.0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    s += p[i];
+  if (s == 12345.678) out[blockIdx.x] = s;  // never true for the zero buffer: keeps the loads
+}
+
 int main(int argc, char **argv) {
   if (argc < 2) {
-    fprintf(stderr, "usage: %s matrix.bin [iters]\n", argv[0]);
+    fprintf(stderr, "usage: %s matrix.bin [iters] [cold_iters] [dump_prefix]\n", argv[0]);
     return 1;
   }
   const int iters = argc > 2 ? atoi(argv[2]) : 30;
+  const int cold_iters = argc > 3 ? atoi(argv[3]) : 0;
+  const char *dump = argc > 4 ? argv[4] : nullptr;
   hspmv_csr_buf A;
   hspmv_csr3_buf maps;
   if (hspmv_load_bin(argv[1], &A, &maps) != HSPMV_OK) {
@@ -83,10 +94,13 @@ int main(int argc, char **argv) {
   hipStream_t st;
   HIPCK(hipStreamCreate(&st));
 
-  // libhspmv on the same device arrays (borrowed)
-  hspmv_csr dv = {A.m, A.n, A.nnz, d_rp, d_ci, d_val, A.dtype};
+  // libhspmv as the bench runs it: the same matrix with its CSR-3 maps (if
+  // the .bin carries them), planner's choice of kernel, bound to the same
+  // device x and its own y
+  hspmv_csr hv = {A.m, A.n, A.nnz, A.row_ptr, A.col_idx, A.val, A.dtype};
+  hspmv_csr3_maps mv = {maps.n_ssr, maps.n_sr, maps.outer, maps.inner};
   hspmv_handle *h = nullptr;
-  if (hspmv_create_on_device(&h, &dv, nullptr, 0, st, HSPMV_FLAG_DEVICE_PTRS) != HSPMV_OK) {
+  if (hspmv_create_on_device(&h, &hv, maps.n_ssr > 0 ? &mv : nullptr, 0, st, 0) != HSPMV_OK) {
     fprintf(stderr, "hspmv: %s\n", hspmv_last_error());
     return 1;
   }
@@ -114,10 +128,27 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   HIPCK(hipEventCreate(&e0));
   HIPCK(hipEventCreate(&e1));
-  auto timed = [&](auto launch) {
-    for (int i = 0; i < 5; ++i) launch();
+  // cold: a 512 MiB read before each launch evicts the 256 MiB Infinity
+  // Cache (the same flush for both implementations)
+  const size_t flush_bytes = (size_t)512 << 20;
+  void *fa = nullptr, *fb = nullptr;
+  if (cold_iters > 0) {
+    HIPCK(hipMalloc(&fa, flush_bytes));
+    HIPCK(hipMalloc(&fb, 4096 * sizeof(double)));
+    HIPCK(hipMemset(fa, 0, flush_bytes));
+    HIPCK(hipDeviceSynchronize());
+  }
+  auto timed = [&](auto launch, int n, bool cold) {
+    if (!cold)
+      for (int i = 0; i < 5; ++i) launch();
     std::vector<double> t;
-    for (int i = 0; i < iters; ++i) {
+    for (int i = 0; i < n; ++i) {
+      if (cold) {
+        hipLaunchKernelGGL(flush_read, dim3(4096), dim3(256), 0, st, (const double *)fa,
+                           flush_bytes / sizeof(double), (double *)fb);
+        HIPCK(hipGetLastError());
+        HIPCK(hipStreamSynchronize(st));
+      }
       HIPCK(hipEventRecord(e0, st));
       launch();
       HIPCK(hipEventRecord(e1, st));
@@ -129,17 +160,31 @@ int main(int argc, char **argv) {
     std::sort(t.begin(), t.end());
     return std::make_pair(t[0], t[t.size() / 2]);
   };
+  auto dump_y = [&](const char *tag, const std::vector<char> &y) {
+    if (!dump) return;
+    std::string path = std::string(dump) + "_" + tag + ".bin";
+    FILE *fp = fopen(path.c_str(), "wb");
+    if (!fp || fwrite(y.data(), 1, y.size(), fp) != y.size()) {
+      fprintf(stderr, "cannot write %s\n", path.c_str());
+      exit(1);
+    }
+    fclose(fp);
+  };
 
   // libhspmv reference timing + y
-  auto th = timed([&] { hspmv_spmv(h); });
+  auto th = timed([&] { hspmv_spmv(h); }, iters, false);
+  auto thc = cold_iters > 0 ? timed([&] { hspmv_spmv(h); }, cold_iters, true) : std::make_pair(0.0, 0.0);
   std::vector<char> yh(sv * A.m), ys(sv * A.m);
   HIPCK(hipStreamSynchronize(st));
   HIPCK(hipMemcpy(yh.data(), d_y2, sv * A.m, hipMemcpyDeviceToHost));
-  static const char *kn[] = {"auto", "vector", "stream", "csr3"};
+  dump_y("hspmv", yh);
+  static const char *kn[] = {"auto", "vector", "stream", "csr3", "csort"};
   printf("{\"impl\": \"hspmv\", \"kernel\": \"%s\", \"chunk_u\": %d, \"m\": %lld, \"nnz\": %lld, "
-         "\"dtype\": \"%s\", \"t_min_us\": %.3f, \"t_med_us\": %.3f, \"gbps_min\": %.1f}\n",
-         kn[info.kernel & 3], info.chunk_u, (long long)A.m, (long long)A.nnz, f64 ? "f64" : "f32",
-         th.first * 1e6, th.second * 1e6, alg / th.first * 1e-9);
+         "\"dtype\": \"%s\", \"t_min_us\": %.3f, \"t_med_us\": %.3f, \"gbps_min\": %.1f, "
+         "\"cold_med_us\": %.3f}\n",
+         kn[(info.kernel >= 0 && info.kernel <= 4) ? info.kernel : 0], info.chunk_u, (long long)A.m,
+         (long long)A.nnz, f64 ? "f64" : "f32", th.first * 1e6, th.second * 1e6,
+         alg / th.first * 1e-9, thc.second * 1e6);
   fflush(stdout);
 
   // per-row |a x| sums for the comparison
@@ -177,12 +222,15 @@ int main(int argc, char **argv) {
       if (buf) HIPCK(hipFree(buf));
       continue;
     }
-    auto tt = timed([&] {
+    auto run_sp = [&] {
       SPCK(hipsparseSpMV(sp, HIPSPARSE_OPERATION_NON_TRANSPOSE, alpha, mat, vx, beta, vy, dt, a.alg,
                          buf));
-    });
+    };
+    auto tt = timed(run_sp, iters, false);
+    auto ttc = cold_iters > 0 ? timed(run_sp, cold_iters, true) : std::make_pair(0.0, 0.0);
     HIPCK(hipStreamSynchronize(st));
     HIPCK(hipMemcpy(ys.data(), d_y, sv * A.m, hipMemcpyDeviceToHost));
+    dump_y(a.name, ys);
     double maxrel = 0.0;
     for (int64_t r = 0; r < A.m; ++r) {
       const double a1 = f64 ? ((double *)yh.data())[r] : ((float *)yh.data())[r];
@@ -192,13 +240,17 @@ int main(int argc, char **argv) {
     }
     printf("{\"impl\": \"hipsparse\", \"alg\": \"%s\", \"m\": %lld, \"nnz\": %lld, \"dtype\": \"%s\", "
            "\"t_min_us\": %.3f, \"t_med_us\": %.3f, \"gbps_min\": %.1f, \"hspmv_speedup\": %.3f, "
-           "\"max_rel_diff_vs_hspmv\": %.3e, \"preprocess_status\": %d}\n",
+           "\"max_rel_diff_vs_hspmv\": %.3e, \"preprocess_status\": %d, \"cold_med_us\": %.3f, "
+           "\"hspmv_speedup_cold\": %.3f}\n",
            a.name, (long long)A.m, (long long)A.nnz, f64 ? "f64" : "f32", tt.first * 1e6,
-           tt.second * 1e6, alg / tt.first * 1e-9, tt.first / th.first, maxrel, (int)pst);
+           tt.second * 1e6, alg / tt.first * 1e-9, tt.first / th.first, maxrel, (int)pst,
+           ttc.second * 1e6, thc.second > 0 ? ttc.second / thc.second : 0.0);
     fflush(stdout);
     if (buf) HIPCK(hipFree(buf));
   }
   hspmv_destroy(h);
   hipsparseDestroy(sp);
+  if (fa) HIPCK(hipFree(fa));
+  if (fb) HIPCK(hipFree(fb));
   return 0;
 }

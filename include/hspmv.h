@@ -50,8 +50,14 @@ extern "C" {
 /* ---------------------------------------------------------------- types */
 typedef enum { HSPMV_F32 = 0, HSPMV_F64 = 1 } hspmv_dtype;
 
-/* A CSR matrix.  Borrowed: the library copies (or, with
- * HSPMV_FLAG_DEVICE_PTRS, references) the arrays during hspmv_create only. */
+/* A CSR matrix.  Borrowed: hspmv_create copies host arrays (the caller may
+ * free them afterwards).  With HSPMV_FLAG_DEVICE_PTRS the handle REFERENCES
+ * the caller's device arrays: they must stay allocated and unchanged for the
+ * handle's lifetime -- the row kernels read row_ptr / col_idx / val on every
+ * SpMV, and the derived tables built at creation (16-bit columns, x
+ * dictionaries, x slabs, column-sorted blocks) are snapshots of col_idx and
+ * val, so an in-place update would be used partly or not at all.  Re-create
+ * the handle after changing the matrix. */
 typedef struct {
   int64_t m, n, nnz;
   const int32_t *row_ptr; /* m+1 entries, row_ptr[0] == 0                */
@@ -166,7 +172,9 @@ typedef struct hspmv_handle hspmv_handle;
                                              the row kernels (see below)   */
 #define HSPMV_FLAG_NONTEMPORAL (1u << 12) /* nt loads for val/col streams  */
 #define HSPMV_FLAG_DEVICE_PTRS (1u << 13) /* A/maps are device pointers on
-                                             the target device (borrowed)  */
+                                             the target device (borrowed for
+                                             the handle's lifetime, unchanged;
+                                             see hspmv_csr)                 */
 #define HSPMV_FLAG_NO_XCD_REMAP (1u << 14) /* keep dispatch-order blocks    */
 /* Default (neither XCD flag): remap only when the matrix's bytes fit the
  * 256 MiB Infinity Cache (<= 192 MiB), where per-XCD L2 reuse of x pays;
@@ -211,6 +219,15 @@ typedef struct hspmv_handle hspmv_handle;
  * the H2D uploads of csrk.cu:580-587 / 847-865 and cuda-spmv-csr/spmv.cu:66-71. */
 int hspmv_create(hspmv_handle **h, const hspmv_csr *A,
                  const hspmv_csr3_maps *maps, int num_gpus, unsigned flags);
+
+/* The row-range partition of hspmv_create over an explicit device list:
+ * shard p lives on devices[p] (n_shards >= 1; a device may repeat).  Distinct
+ * devices exchange x / y through RCCL (ncclCommInitAll over the list, also
+ * at n_shards = 1); a list that repeats a device exchanges by device-to-
+ * device copies.  hspmv_create(num_gpus > 1) is this with devices 0..P-1. */
+int hspmv_create_sharded(hspmv_handle **h, const hspmv_csr *A,
+                         const hspmv_csr3_maps *maps, const int *devices,
+                         int n_shards, unsigned flags);
 
 /* Single-device handle on `device`, launching on `stream` (a hipStream_t;
  * NULL = the library creates one).  This is the entry a one-process-per-GPU

@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, config, q):
+def _worker(rank, world, port, config, q, use_hip=False):
     sys.path.insert(0, str(REPO / "heterogeneous-spmv_amd"))
     sys.path.insert(0, str(REPO / "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -40,7 +40,12 @@ def _worker(rank, world, port, config, q):
             x.copy_(torch.from_numpy(gen.rand_x(sh.n_global, 42)))
         hdist.broadcast_x(x)
         xn = x.numpy()
-        y_local = oracle.spmv(sh.A.row_ptr, sh.A.col_idx, sh.A.val, xn)
+        if use_hip:  # the rank's shard through the HIP library (C ABI), device 0
+            import hspmv
+            with hspmv.SpMV(sh.A, device=0) as op:
+                y_local = op(xn)
+        else:
+            y_local = oracle.spmv(sh.A.row_ptr, sh.A.col_idx, sh.A.val, xn)
         ok, rel = hdist.checksum_ok(sh.A, xn, y_local)
         y = hdist.gather_y(torch.from_numpy(y_local), sh.splits).numpy()
         nnz = torch.tensor([sh.A.nnz], dtype=torch.int64)
@@ -51,15 +56,15 @@ def _worker(rank, world, port, config, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_row_range_partition_gloo(world):
+def _run_partition(world, use_hip):
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
     from hspmv import gen
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, "small", q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "small", q, use_hip))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -77,6 +82,20 @@ def test_row_range_partition_gloo(world):
     assert splits[0] == 0 and splits[-1] == A.m and np.all(np.diff(splits) > 0)
     shard_nnz = A.row_ptr[splits[1:]] - A.row_ptr[splits[:-1]]
     assert shard_nnz.max() - shard_nnz.min() <= 10     # nnz-balanced
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_range_partition_gloo(world):
+    _run_partition(world, use_hip=False)
+
+
+@pytest.mark.gpu
+def test_row_range_partition_gloo_hip_ranks():
+    """The same orchestration with every rank's y from the HIP library on
+    device 0 (gloo for the exchanges; the oracle only checks): the STREAM
+    kernel's y is bit-identical to omp_spmv on these rows, so the gathered y
+    equals the oracle exactly."""
+    _run_partition(2, use_hip=True)
 
 
 def test_weak_scaling_shards_have_equal_work():
