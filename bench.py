@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "vector", "csr3"])
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--nt", action="store_true", help="non-temporal matrix loads")
+    ap.add_argument("--xcd-chunk", type=int, default=0,
+                    help="workgroups per XCD turn (0 = the planner's choice, 1 = dispatch order)")
     ap.add_argument("--cold-steps", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-baseline sample (rank 0, N=1)")
@@ -291,7 +293,9 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     op = hspmv.SpMV(A, maps, device=local, stream=stream.cuda_stream, kernel=args.kernel,
-                    lanes=args.lanes, nontemporal=args.nt)
+                    lanes=args.lanes, nontemporal=args.nt,
+                    xcd_remap=(False if args.xcd_chunk == 1 else None),
+                    xcd_chunk=(args.xcd_chunk if args.xcd_chunk > 1 else 0))
     info = op.info
 
     # x: generated on rank 0, broadcast over RCCL (the path's exchange step)
@@ -393,9 +397,14 @@ def main():
 
     if rank == 0:
         ctype = "double" if np_dt == np.float64 else "float"
-        kname = {"csr3": "hspmv_csr3", "stream": "hspmv_csr_stream",
+        kname = {"csr3": "hspmv_csr3", "stream": "hspmv_csr_stream", "csort": "hspmv_csort",
                  "vector": "hspmv_csr_vector"}.get(info["kernel_name"], info["kernel_name"])
-        launches = info["x_slabs"] or 1
+        csort = info["kernel_name"] == "csort"
+        launches = 1 if csort else (info["x_slabs"] or 1)
+        # csort: the finishing pass (column parts / long-row slices) unless the
+        # block sums are written to y directly (one part, no long rows)
+        extra = (0 if (info["csort_parts"] == 1 and not info["n_split_rows"]) else 1) if csort else \
+            (2 if info["n_split_rows"] else 0)
         out = {
             "metric": METRIC,
             "value": round(gflops, 3),
@@ -414,6 +423,7 @@ def main():
                        "csr3_maps": ({"n_ssr": maps.n_ssr, "n_sr": maps.n_sr} if maps is not None
                                      else None),
                        "kernel": info["kernel_name"], "chunk_u": info["chunk_u"],
+                       "xcd_chunk": info["xcd_remap"],
                        "x_dict": info["x_dict"], "x_windows": info["x_windows"],
                        "x_slabs": info["x_slabs"], "col16": info["col16"],
                        "nontemporal": bool(args.nt), "parallelism": f"row-range x{world}",
@@ -424,7 +434,10 @@ def main():
                          "traffic": (traffic["hbm_bytes_per_launch"] if traffic else None),
                          "kernel": f"{kname}<{ctype},...>",
                          "row_kernel_launches_per_spmv": launches,
-                         "split_row_launches_per_spmv": 2 if info["n_split_rows"] else 0,
+                         "split_row_launches_per_spmv": 0 if csort else extra,
+                         "finish_launches_per_spmv": extra if csort else 0,
+                         "launches_per_spmv": launches + extra,
+                         "csort_parts": info["csort_parts"],
                          "alg_bytes_per_launch": alg_local,
                          "format_bytes_per_launch": info["format_bytes"],
                          "launch_us_events": round(ev_launch_s * 1e6, 3),

@@ -1096,6 +1096,7 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
     s.h_xwin_t.clear();
     s.A.col_span_bits = 1;
     s.A.has_xdict = s.xd_shape == kStream;
+    s.A.has_xdict_tasks = s.xd_shape == kCsr3;
     return HSPMV_OK;
   }
   s.A.has_xwin = !s.h_xwin.empty();

@@ -30,6 +30,7 @@ struct DevCSR {
   // planner hints from the host tables: STREAM x windows / block x
   // dictionaries were built for this shard
   bool has_xwin = false, has_xdict = false;
+  bool has_xdict_tasks = false;  // x dictionaries built for packed CSR3 tasks
   int32_t n_slabs = 1;        // x slabs: the row kernel's passes (each sees ~nnz / n_slabs)
   int32_t task_waves = 4;     // CSR3 packed tasks per workgroup (4, or 8 with x dictionaries)
   bool has_csort = false;     // column-sorted row blocks were built (irregular gathers)

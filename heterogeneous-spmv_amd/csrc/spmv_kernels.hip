@@ -258,8 +258,14 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
     chunk = 1;
   else if (flags & (1u << 22))  // HSPMV_FLAG_XCD_REMAP
     full = true;
-  else
-    full = footprint <= 192.0 * 1024 * 1024;
+  else if (footprint <= 192.0 * 1024 * 1024)
+    full = true;
+  else if (A.has_xdict || A.has_xdict_tasks)
+    // x dictionaries: each XCD takes 4 consecutive workgroups in turn, so the
+    // x runs neighbouring workgroups stage are still in that XCD's L2
+    // (C3 CSR-3 fp64 112.7 -> 105.2 us, fp32 63.7 -> 62.6; 2 / 8 / 16 / 64
+    // blocks: 112.3 / 105.8 / 109.4 / 109.6; profiles/r02k_ab_xcd.jsonl)
+    chunk = 4;
   if (k == kAuto)
     p.kernel = A.has_csort ? kCsort : ((A.n_ssr > 0) ? kCsr3 : kStream);
   else

@@ -65,10 +65,17 @@ def main():
     ap.add_argument("--last", type=int, default=0, help="use only the last N dispatches")
     ap.add_argument("--skip-last", type=int, default=0, help="drop the last N dispatches")
     ap.add_argument("--alg-bytes", type=float, default=0.0)
+    ap.add_argument("--per-spmv", type=int, default=1,
+                    help="consecutive matching dispatches that form one SpMV (summed)")
+    ap.add_argument("--extra", default="",
+                    help="a pass with any other counters: each is reported per SpMV")
     ap.add_argument("-o", "--out", required=True)
     a = ap.parse_args()
     fc, wc = find_csv(a.fetch), find_csv(a.write)
+    K = max(1, a.per_spmv)
+
     def sel(v):
+        v = [sum(v[i:i + K]) for i in range(0, len(v) - K + 1, K)]
         v = v[a.skip_first:]
         if a.skip_last:
             v = v[:-a.skip_last]
@@ -104,6 +111,21 @@ def main():
                                   "(size-resolved fabric reads, calibrated on a known byte count)",
                     "source": f"rocprofv3 --pmc TCC_EA0_RDREQ_{{128B,64B,32B}}_sum ({rc.name}) / "
                               f"--pmc WRITE_SIZE ({wc.name}); FETCH_SIZE ({fc.name}) kept as hbm_bytes_guide"})
+    if a.extra:
+        ec = find_csv(a.extra)
+        names = set()
+        with open(ec) as f:
+            for row in csv.DictReader(f):
+                if a.kernel_substr in row.get("Kernel_Name", ""):
+                    names.add(row["Counter_Name"])
+        ex = {}
+        for nm in sorted(names):
+            v = sel(per_dispatch(ec, nm, a.kernel_substr))
+            if v:
+                ex[nm] = sum(v) / len(v)
+        out["extra_counters_per_spmv"] = ex
+        out["extra_source"] = ec.name
+    out["dispatches_per_spmv"] = K
     hbm = out["hbm_bytes_per_launch"]
     if a.alg_bytes:
         out["alg_bytes_per_launch"] = a.alg_bytes

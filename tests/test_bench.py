@@ -89,6 +89,7 @@ def test_bench_json_line_contract():
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert r["kernel"].startswith("hspmv_csr3<double")
+    assert r["launches_per_spmv"] == 1 and r["csort_parts"] == 0
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
     assert abs(c["value"] - 2 * d["config"]["nnz"] / c["time_min_s"] * 1e-9) < 1e-2 * c["value"]
