@@ -371,6 +371,14 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   if (!p.nontemporal && hbm && A.col_span_bits > 17 && (double)A.n * sv > 4.0 * 1024 * 1024 &&
       A.n_slabs <= 1)
     p.nontemporal = true;
+  // fp64 CSR3 tasks with x dictionaries: the next chunk's col/val loads are
+  // issued during this chunk's gathers and sums (C3 112.2 -> 105.8 us on one
+  // box, 112.4 -> 110.3 on another; slower everywhere else: C3 fp32 +14 %,
+  // C4 +13 %, honeycomb +10 %, C2 +14 %; profiles/r02q_ab_c3_u.jsonl,
+  // r02r_ab_pf.jsonl)
+  if (!p.prefetch && dtype == 1 && p.kernel == kCsr3 && A.has_xdict_tasks && !forced_u)
+    p.prefetch = true;
+  if (const char *e = getenv("HSPMV_PF")) p.prefetch = atoi(e) != 0;
   if (const char *e = getenv("HSPMV_YNT")) p.y_nt = atoi(e) != 0;
   if (const char *e = getenv("HSPMV_NT")) p.nontemporal = atoi(e) != 0;
   if (const char *e = getenv("HSPMV_DYNLDS")) p.dyn_lds = atoi(e);
