@@ -74,6 +74,11 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
                     help="print the workload and partition plan, touch no GPU")
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0,
+    # gloo for the exchanges (RCCL allows one rank per device); never the
+    # driver's configuration
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help=argparse.SUPPRESS)
+    ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
     if a.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -114,10 +119,15 @@ def dist_setup(args):
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP GPU")
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     return rank, world, local
 
 
@@ -134,7 +144,8 @@ def reduce_over_ranks(v: float, world: int, op: str) -> float:
         return v
     import torch
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return float(t.item())
 

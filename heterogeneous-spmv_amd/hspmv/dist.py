@@ -191,10 +191,21 @@ def build_shard(config: str, rank: int, world: int, dtype=None) -> Shard:
 
 # ------------------------------------------------------------------ exchanges
 
+def _staged(t):
+    """gloo moves host tensors only: a device tensor goes through a host copy
+    (the one-GPU rehearsal of the multi-rank path); under "nccl" (RCCL) the
+    tensor is used as it is."""
+    import torch.distributed as dist
+    return t.cpu() if (t.is_cuda and dist.get_backend() != "nccl") else t
+
+
 def broadcast_x(x, src: int = 0) -> None:
     """In-place broadcast of the full x (a torch tensor) from rank src."""
     import torch.distributed as dist
-    dist.broadcast(x, src)
+    xs = _staged(x)
+    dist.broadcast(xs, src)
+    if xs is not x:
+        x.copy_(xs)
 
 
 def gather_y(y_local, splits: np.ndarray):
@@ -207,7 +218,8 @@ def gather_y(y_local, splits: np.ndarray):
     pad = int(rows.max())
     buf = torch.zeros(pad, dtype=y_local.dtype, device=y_local.device)
     buf[: y_local.shape[0]] = y_local
-    out = torch.empty(pad * world, dtype=y_local.dtype, device=y_local.device)
+    buf = _staged(buf)
+    out = torch.empty(pad * world, dtype=y_local.dtype, device=buf.device)
     dist.all_gather_into_tensor(out, buf)
     parts = [out[r * pad: r * pad + int(rows[r])] for r in range(world)]
     return torch.cat(parts)
@@ -286,14 +298,17 @@ def halo_exchange(x_win, halo: Halo) -> None:
     """Fills the non-owned parts of x_win (a torch tensor holding x[lo:hi),
     own part already written) from the ranks that own them."""
     import torch.distributed as dist
+    xw = _staged(x_win)
     ops = []
     for q, g0, g1 in halo.sends:
-        ops.append(dist.P2POp(dist.isend, x_win[g0 - halo.lo:g1 - halo.lo].contiguous(), q))
+        ops.append(dist.P2POp(dist.isend, xw[g0 - halo.lo:g1 - halo.lo].contiguous(), q))
     for q, g0, g1 in halo.recvs:
-        ops.append(dist.P2POp(dist.irecv, x_win[g0 - halo.lo:g1 - halo.lo], q))
+        ops.append(dist.P2POp(dist.irecv, xw[g0 - halo.lo:g1 - halo.lo], q))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+    if xw is not x_win:
+        x_win.copy_(xw)
 
 
 def halo_bytes(halo: Halo, itemsize: int = 8) -> int:

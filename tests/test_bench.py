@@ -99,3 +99,34 @@ def test_bench_json_line_contract():
         assert ref["kind"] == "reference" and ref["value"] > 0 and ref["time_min_s"] > 0
     assert d["cold"]["launch_us"] > 0
     assert d["check"]["pass"] is True
+
+
+@pytest.mark.gpu
+def test_bench_multi_rank_path_rehearsal_on_one_gpu(tmp_path):
+    """bench.py's N > 1 code path (shards, x broadcast, barriers, max over
+    ranks, y all-gather, halo exchange, rank-0 JSON line) run as 2 ranks that
+    share device 0 and exchange over gloo -- RCCL allows one rank per device,
+    so this is the rehearsal a one-GPU box can do; the driver's N > 1 runs use
+    RCCL on one GPU per rank.  C2 (weak scaling) keeps it short."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                          "--master-port", str(port), str(REPO / "bench.py"), "--gpus", "2",
+                          "--backend", "gloo", "--same-device", "--config", "c2",
+                          "--steps", "10", "--warmup", "2", "--cold-steps", "2"],
+                         cwd=REPO, env=env, capture_output=True, text=True, timeout=400)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["check"]["pass"] is True
+    assert d["config"]["m"] == 2_000_000 and d["config"]["parallelism"] == "row-range x2"
+    c = d["comm"]
+    assert c["bcast_x_ms"] > 0 and c["gather_y_ms"] > 0 and c["halo_x_ms"] > 0
+    assert c["halo_bytes_per_rank"] == 1000 * 8   # one grid line from the neighbour
+    assert d["cpu_baseline"] is None              # rank 0 at N = 1 only
