@@ -28,6 +28,8 @@ Extra fields on the line:
                every launch (a 512 MiB read)
   comm         RCCL x broadcast / y all-gather / halo-exchange times (N > 1),
                timed separately, and the end-to-end rates they imply
+  scaling_reference  (N = 1) the N > 1 default workload, C4, timed on this
+               one GPU: the same-matrix N = 1 point for the strong-scaling curve
   cpu_baseline the oracle's OpenMP restatement of spmv-csr's omp_spmv on the
                host cores, on the SAME matrix (rank 0 at N = 1 only, bounded
                sample), value from TimeMin as run_norm.py records it; beside
@@ -45,7 +47,12 @@ import sys
 import time
 from pathlib import Path
 
-os.environ.setdefault("OMP_SCHEDULE", "static")  # before any libgomp loads
+# before any libgomp loads: the CPU baseline's schedule (run_norm.py:18,66).
+# OMP_PROC_BIND / OMP_PLACES are NOT set: libgomp then pins
+# the main thread to one core at load, which shrinks the affinity mask the
+# baseline reads its thread count from to that core (r02x: 2 threads,
+# 11.5 GFLOP/s instead of 128 threads, 144 GFLOP/s).
+os.environ.setdefault("OMP_SCHEDULE", "static")
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "heterogeneous-spmv_amd"))
@@ -72,6 +79,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-scaling-ref", action="store_true",
+                    help="at N = 1, skip timing the N > 1 configuration (C4) on this GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="print the workload and partition plan, touch no GPU")
     # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0,
@@ -280,6 +289,48 @@ def reference_cpu(A, x, threads: int, budget_s: float):
                        f"{len(ts)} timed calls, value = 2 nnz / TimeMin")}
 
 
+def scaling_reference(args, stream):
+    """The N > 1 default workload (C4, the whole 200 M-nnz banded matrix) on
+    this one GPU, same protocol as the step: the same-configuration N = 1
+    point of a strong-scaling curve whose N > 1 points bench.py reports
+    (the N = 1 headline is C3, a different matrix)."""
+    import torch
+
+    import hspmv
+    from hspmv import dist as hdist
+    from hspmv import gen
+    cfg = hdist.default_config(2)
+    sh = hdist.build_shard(cfg, 0, 1)
+    A = sh.A
+    op = hspmv.SpMV(A, None, device=torch.cuda.current_device(), stream=stream.cuda_stream)
+    x = torch.from_numpy(gen.rand_x(sh.n_global, 42)).to("cuda")
+    y = torch.empty(A.m, dtype=x.dtype, device="cuda")
+    op.bind_x_device(x.data_ptr())
+    op.bind_y_device(y.data_ptr())
+    for _ in range(max(3, args.warmup // 4)):
+        op.spmv()
+    steps = max(10, args.steps // 10)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        op.spmv()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    step_s = (time.perf_counter() - t0) / steps
+    ev_s = ev0.elapsed_time(ev1) * 1e-3 / steps
+    info = op.info
+    op.close()
+    return {"config": f"{cfg}: {sh.name}", "n_gpus": 1, "m": sh.m_global, "nnz": sh.nnz_global,
+            "value": round(2.0 * sh.nnz_global / step_s * 1e-9, 3), "unit": "GFLOP/s",
+            "ms_per_step": round(step_s * 1e3, 6), "steps": steps,
+            "launch_us_events": round(ev_s * 1e6, 3), "kernel": info["kernel_name"],
+            "frac": round(info["alg_bytes"] / ev_s * 1e-9 / HBM_PEAK_GBS, 4),
+            "note": ("the N > 1 default workload on this one GPU: an N-GPU run of it "
+                     "(bench.py --gpus N) over N x this value is its strong-scaling efficiency")}
+
+
 # ------------------------------------------------------------------ main
 
 def main():
@@ -401,6 +452,10 @@ def main():
     workload_key = f"{cfg}-w{world}-r0-{info['kernel_name']}"
     traffic = load_traffic(workload_key) if rank == 0 else None
 
+    sref = None
+    if world == 1 and cfg != hdist.default_config(2) and not args.no_scaling_ref:
+        sref = scaling_reference(args, stream)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu, threads = cpu_baseline(A, x_host, args.cpu_seconds)
@@ -471,6 +526,7 @@ def main():
                      "iterative_gflops": (round(flops_step / (step_s + halo_ms * 1e-3) * 1e-9, 3)
                                           if halo_ms is not None else round(gflops, 3))},
             "check": {"pass": bool(ok_all), "checksum_rel": rel},
+            "scaling_reference": sref,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -541,7 +541,7 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
   const ColSrc cs = col_src(A);
   const XDict xd{dp.xd_blk, reinterpret_cast<const int2 *>(dp.xd_runs)};
   // dynamic LDS: the block's x dictionary (XD), or occupancy experiments (HSPMV_DYNLDS)
-  const unsigned dyn = XD ? (unsigned)dp.xd_lds_bytes : (unsigned)p.dyn_lds;
+  const unsigned dyn = XD ? (unsigned)dp.xd_lds_bytes + (unsigned)p.dyn_lds : (unsigned)p.dyn_lds;
   if (p.kernel == kStream) {
     const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
     if constexpr (XD)

@@ -99,6 +99,8 @@ def test_bench_json_line_contract():
         assert ref["kind"] == "reference" and ref["value"] > 0 and ref["time_min_s"] > 0
     assert d["cold"]["launch_us"] > 0
     assert d["check"]["pass"] is True
+    sr = d["scaling_reference"]  # C4 on this one GPU: the N = 1 point of the N > 1 curve
+    assert sr["config"].startswith("c4") and sr["nnz"] > 199_999_000 and sr["value"] > 0
 
 
 @pytest.mark.gpu
@@ -130,3 +132,4 @@ def test_bench_multi_rank_path_rehearsal_on_one_gpu(tmp_path):
     assert c["bcast_x_ms"] > 0 and c["gather_y_ms"] > 0 and c["halo_x_ms"] > 0
     assert c["halo_bytes_per_rank"] == 1000 * 8   # one grid line from the neighbour
     assert d["cpu_baseline"] is None              # rank 0 at N = 1 only
+    assert d["scaling_reference"] is None
