@@ -188,7 +188,7 @@ __global__ __launch_bounds__(NTH) void csortg_kernel(const int64_t *__restrict__
 // Variant H: 2-D split.  Workgroup b handles row block b / H and column
 // part h = b % H (x[h*N/H, (h+1)*N/H)); its fp64 row sums go to
 // part[h*m + row]; csort_finish adds the H partials per row (fixed order).
-template <int U, int NTH, bool NT, int H>
+template <int U, int NTH, bool NT, int H, typename Acc = double>
 __global__ __launch_bounds__(NTH) void csorth_kernel(const int64_t *__restrict__ blk_k,
                                                      const int32_t *__restrict__ blk_r,
                                                      const int32_t *__restrict__ cbase,
@@ -196,13 +196,13 @@ __global__ __launch_bounds__(NTH) void csorth_kernel(const int64_t *__restrict__
                                                      const float *__restrict__ x, int64_t m,
                                                      double *__restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double *acc = reinterpret_cast<double *>(smem);
+  Acc *acc = reinterpret_cast<Acc *>(smem);
   const int b = blockIdx.x;
   const int rb = b / H, h = b % H;
   const int64_t k0 = blk_k[b], k1 = blk_k[b + 1];
   const int32_t r0 = blk_r[rb], r1 = blk_r[rb + 1];
   const int nr = r1 - r0;
-  for (int i = threadIdx.x; i < nr; i += NTH) acc[i] = 0.0;
+  for (int i = threadIdx.x; i < nr; i += NTH) acc[i] = Acc(0);
   __syncthreads();
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int NW = NTH / 64;
@@ -222,11 +222,11 @@ __global__ __launch_bounds__(NTH) void csorth_kernel(const int64_t *__restrict__
 #pragma unroll
     for (int u = 0; u < U; ++u) xv[u] = x[base + oo[u]];
 #pragma unroll
-    for (int u = 0; u < U; ++u) atomicAdd(&acc[rr[u]], (double)(vv[u] * xv[u]));
+    for (int u = 0; u < U; ++u) atomicAdd(&acc[rr[u]], (Acc)(vv[u] * xv[u]));
   }
   __syncthreads();
   double *out = part + (int64_t)h * m + r0;
-  for (int i = threadIdx.x; i < nr; i += NTH) out[i] = acc[i];
+  for (int i = threadIdx.x; i < nr; i += NTH) out[i] = (double)acc[i];
 }
 
 template <int H>
@@ -594,7 +594,7 @@ int main(int argc, char **argv) {
     if (dv) (void)hipFree(dv);
     if (da) (void)hipFree(da);
   };
-  auto run3 = [&](const char *name, int G, int U, bool nt, int H) {
+  auto run3 = [&](const char *name, int G, int U, bool nt, int H, bool acc32 = false) {
     Blocked B = block_sort(A, G, U, true, true, H);
     const int64_t tot = B.bk[G];
     std::vector<uint64_t> aos((size_t)tot);
@@ -609,20 +609,20 @@ int main(int argc, char **argv) {
     u32x2 *da = reinterpret_cast<u32x2 *>(up(aos));
     double *dpart = nullptr;
     CK(hipMalloc(&dpart, (size_t)H * m * 8));
-    const size_t lds = (size_t)B.max_rows * 8;
+    const size_t lds = (size_t)B.max_rows * (acc32 ? 4 : 8);
     if (lds > 160 * 1024) { printf("{\"name\":\"%s\",\"skip\":\"lds %zu\"}\n", name, lds); return; }
     bool ok = true;
     auto launch = [&]() {
-#define H_(UU, NTL, HH)                                                                       \
-  if (U == UU && nt == NTL && H == HH) {                                                      \
-    hipLaunchKernelGGL((csorth_kernel<UU, 1024, NTL, HH>), dim3(G), dim3(1024), lds, 0, dbk,  \
-                       dbr, dcb, da, dx, m, dpart);                                           \
+#define H_(UU, NTL, HH, AC)                                                                   \
+  if (U == UU && nt == NTL && H == HH && acc32 == (sizeof(AC) == 4)) {                        \
+    hipLaunchKernelGGL((csorth_kernel<UU, 1024, NTL, HH, AC>), dim3(G), dim3(1024), lds, 0,   \
+                       dbk, dbr, dcb, da, dx, m, dpart);                                      \
     hipLaunchKernelGGL((csort_finish<HH>), dim3((unsigned)((m + 255) / 256)), dim3(256), 0, 0, \
                        m, dpart, dy);                                                         \
     return;                                                                                   \
   }
-      H_(4, false, 1) H_(8, false, 1) H_(8, true, 1) H_(4, false, 2) H_(8, false, 2)
-      H_(8, true, 2) H_(16, true, 2) H_(8, true, 4)
+      H_(16, true, 2, double) H_(16, true, 2, float) H_(16, true, 4, float) H_(8, true, 4, float)
+      H_(16, true, 1, double)
 #undef H_
       ok = false;
     };
@@ -656,17 +656,10 @@ int main(int argc, char **argv) {
     (void)hipFree(dbk); (void)hipFree(dbr); (void)hipFree(dcb); (void)hipFree(da);
     (void)hipFree(dpart);
   };
-  run3("h1_U4", 256, 4, false, 1);
-  run3("h1_U8", 256, 8, false, 1);
-  run3("h1_U8_nt", 256, 8, true, 1);
-  run3("h2_U4", 256, 4, false, 2);
-  run3("h2_U8", 256, 8, false, 2);
-  run3("h2_U8_nt", 256, 8, true, 2);
-  run3("h2_U16_nt", 256, 16, true, 2);
-  run2("g_aos", 256, 4, 1024, 2, false, 0);
-  run2("g_aos_nt", 256, 4, 1024, 2, true, 0);
-  run2("g_aos_U8", 256, 8, 1024, 2, false, 0);
-  run2("diag_noatomic", 256, 4, 1024, 2, false, 1);
-  run2("diag_nogather", 256, 4, 1024, 2, false, 2);
+  run3("h2_U16_f64", 256, 16, true, 2);
+  run3("h2_U16_f32", 256, 16, true, 2, true);
+  run3("h4_U16_f32", 256, 16, true, 4, true);
+  run3("h4_U8_f32", 256, 8, true, 4, true);
+  run3("h1_U16_f64", 256, 16, true, 1);
   return 0;
 }

@@ -509,7 +509,8 @@ def test_xdict_bitwise_and_fallback(monkeypatch):
             maps = hspmv.build_csr3_maps(Ad, 20, 10)
             for kw, mp in [(dict(kernel="stream"), None), (dict(kernel="stream", prefetch=True), None),
                            (dict(kernel="csr3"), maps), (dict(kernel="stream", chunk_u=2), None),
-                           (dict(kernel="csr3", nontemporal=True), maps)]:
+                           (dict(kernel="csr3", nontemporal=True), maps),
+                           (dict(kernel="csr3", prefetch=True), maps)]:
                 monkeypatch.setenv("HSPMV_XDICT", "1")
                 yd, idd = gpu_spmv(Ad, x, mp, **kw)
                 monkeypatch.setenv("HSPMV_XDICT", "0")
