@@ -391,6 +391,74 @@ void pack_csr3_tasks(const std::vector<int32_t> &in, int32_t m, std::vector<int3
   ts.push_back(m);
 }
 
+// Heavy tasks.  A wave's task is also capped at a nonzero budget (in-kernel
+// rows only: split rows are summed elsewhere), cut at row boundaries: with
+// 64 rows of 512-2048 nonzeros one wave would stream 32-128 K nonzeros and a
+// 25 K-row matrix would fill only 381 waves (d2048: 3.9 ms against 120 us
+// for a wave per row, profiles/r02z2_ab_vector.jsonl).  HSPMV_TASK_NNZ moves
+// the budget.
+constexpr int32_t kTaskNnz = 2048;
+
+int32_t task_nnz_budget() {
+  const char *e = getenv("HSPMV_TASK_NNZ");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : kTaskNnz;
+}
+
+void cap_task_nnz(const int32_t *rp, int32_t long_t, int32_t budget, std::vector<int32_t> &ts) {
+  std::vector<int32_t> out;
+  out.reserve(ts.size());
+  for (size_t t = 0; t + 1 < ts.size(); ++t) {
+    const int32_t a = ts[t], b = ts[t + 1];
+    out.push_back(a);
+    int64_t acc = 0;
+    for (int32_t r = a; r < b; ++r) {
+      const int64_t len = rp[r + 1] - rp[r] > long_t ? 0 : rp[r + 1] - rp[r];
+      if (r > out.back() && acc + len > budget) {
+        out.push_back(r);
+        acc = 0;
+      }
+      acc += len;
+    }
+  }
+  out.push_back(ts.back());
+  ts.swap(out);
+}
+
+// The wave tasks of a shard (empty: STREAM's fixed 64-row groups, or the
+// workgroup-per-super-super-row CSR-3 plan).  CSR-3: the packed super-rows.
+// CSR under the auto (or CSR3) kernel: when at least a quarter of the
+// in-kernel nonzeros sit in 64-row groups over the budget, the 64-row groups
+// with the heavy ones cut -- the CSR3 kernel then runs them (a CSR-2 with
+// one-row super-rows).  Both are capped at the budget.
+void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner, unsigned flags,
+                 std::vector<int32_t> &ts) {
+  ts.clear();
+  if (!csr3_packed()) return;
+  const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
+  const int32_t budget = task_nnz_budget();
+  if (inner) {
+    pack_csr3_tasks(*inner, (int32_t)m, ts);
+  } else {
+    const unsigned k = flags & 0xFu;
+    if ((k != kAuto && k != kCsr3) || m == 0) return;
+    int64_t heavy = 0, total = 0;
+    for (int64_t g = 0; g < m; g += 64) {
+      int64_t in = 0;
+      for (int64_t r = g; r < std::min(m, g + 64); ++r) {
+        const int64_t len = rp[r + 1] - rp[r];
+        in += len > long_t ? 0 : len;
+      }
+      total += in;
+      heavy += in > budget ? in : 0;
+    }
+    if (4 * heavy < total || heavy == 0) return;
+    for (int64_t g = 0; g < m; g += 64) ts.push_back((int32_t)g);
+    ts.push_back((int32_t)m);
+  }
+  cap_task_nnz(rp, long_t, budget, ts);
+}
+
 // x windows of row groups [starts[g], starts[g+1]) -- the 64-row groups of
 // STREAM when starts is null, the packed CSR-3 tasks otherwise: {lo, w}
 // when the group's columns span w <= kXWin entries, else {0, 0}.  Empty
@@ -461,6 +529,7 @@ int kernel_for_tables(int64_t n_ssr, bool have_tasks, unsigned flags) {
   if (k == kVector) return kVector;
   if ((k == kCsr3 || k == kAuto) && n_ssr > 0)
     return have_tasks ? kCsr3 : -1;  // workgroup-per-SSR plan: no dictionaries
+  if ((k == kCsr3 || k == kAuto) && have_tasks) return kCsr3;  // CSR with heavy groups
   return kStream;
 }
 
@@ -1060,8 +1129,7 @@ int csort_mode() {
 // kernels.
 int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
                      int64_t n, int dtype, unsigned flags) {
-  s.h_tasks.clear();
-  if (s.A.n_ssr > 0 && csr3_packed()) pack_csr3_tasks(s.h_inner, s.A.m, s.h_tasks);
+  build_tasks(rp, m, s.A.n_ssr > 0 ? &s.h_inner : nullptr, flags, s.h_tasks);
   s.h_xwin.clear();
   s.h_xwin_t.clear();
   int rc;
@@ -1859,8 +1927,12 @@ int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, unsigned f
   if ((rc = validate_host_maps(maps, A->m))) return rc;
   std::vector<int32_t> tasks;
   const bool csr3 = maps && maps->n_ssr > 0;
-  if (csr3 && csr3_packed())
-    pack_csr3_tasks(std::vector<int32_t>(maps->inner, maps->inner + maps->n_sr + 1), (int32_t)A->m, tasks);
+  if (csr3) {
+    const std::vector<int32_t> inner(maps->inner, maps->inner + maps->n_sr + 1);
+    build_tasks(A->row_ptr, A->m, &inner, flags, tasks);
+  } else {
+    build_tasks(A->row_ptr, A->m, nullptr, flags, tasks);
+  }
   const int kern = kernel_for_tables(csr3 ? maps->n_ssr : 0, !tasks.empty(), flags);
   if ((kern != kStream && kern != kCsr3) || A->m == 0) return HSPMV_OK;
   if (cap_entries <= 0) cap_entries = xdict_cap_entries(A->dtype);

@@ -67,6 +67,44 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// One DPP move of v (both dwords for fp64); lanes the pattern does not feed
+// read 0.
+template <int CTRL, int ROW_MASK, typename T>
+__device__ __forceinline__ T dpp_move(T v) {
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROW_MASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+    return __builtin_bit_cast(T, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  } else {
+    return __builtin_bit_cast(
+        T, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, false));
+  }
+}
+
+// Wave sum by DPP (row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast 15/31 across rows: an inclusive scan whose lane 63 holds the
+// total), returned wave-uniform.  No LDS round trips, unlike __shfl_xor
+// (ds_bpermute): the cooperative rows' reductions are on the critical path
+// of each chunk (mid-density rows, profiles/r02z*).
+template <typename T>
+__device__ __forceinline__ T wave_sum_dpp(T v) {
+  v += dpp_move<0x111, 0xf>(v);
+  v += dpp_move<0x112, 0xf>(v);
+  v += dpp_move<0x114, 0xf>(v);
+  v += dpp_move<0x118, 0xf>(v);
+  v += dpp_move<0x142, 0xa>(v);
+  v += dpp_move<0x143, 0xc>(v);
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)b, 63);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 63);
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+  }
+}
+
 // Bijective XCD-aware block order (cdna_hip_programming.md §5 "XCD swizzle
 // must be bijective").  Blocks b and b+8 share an XCD under round-robin
 // dispatch; with chunk s > 1 each XCD takes s consecutive logical blocks in
@@ -305,16 +343,18 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         } else {
           if (mine) acc = ordered_sum(acc, lds - c, max(beg, c), min(end, c + last + 1));
         }
-        unsigned long long cm = coop;
+        // only the cooperative rows this chunk touches (rows are contiguous:
+        // the others would add nothing), bounds by readlane (scalar)
+        unsigned long long cm = coop ? coop & __ballot(end > c && beg <= c + last) : 0ull;
         while (cm) {
           const int r = __ffsll(cm) - 1;
           cm &= cm - 1;
-          const int32_t lo = max(__shfl(beg, r, kWave), c);
-          const int32_t hi = min(__shfl(end, r, kWave), c + last + 1);
+          const int32_t lo = max(__builtin_amdgcn_readlane(beg, r), c);
+          const int32_t hi = min(__builtin_amdgcn_readlane(end, r), c + last + 1);
           if (lo < hi) {  // wave-uniform
             T s = T(0);
             for (int32_t k = lo + lane; k < hi; k += kWave) s += lds[k - c];
-            s = wave_sum(s);
+            s = wave_sum_dpp(s);
             if (lane == r) acc += s;
           }
         }

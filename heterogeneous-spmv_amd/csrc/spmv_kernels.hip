@@ -266,12 +266,15 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
     // (C3 CSR-3 fp64 112.7 -> 105.2 us, fp32 63.7 -> 62.6; 2 / 8 / 16 / 64
     // blocks: 112.3 / 105.8 / 109.4 / 109.6; profiles/r02k_ab_xcd.jsonl)
     chunk = 4;
+  // (packed tasks without super-super-rows: a CSR matrix whose 64-row
+  // groups exceed the task budget, hspmv_api.cpp build_tasks)
+  const bool tasks = A.n_ssr > 0 || packed_tasks > 0;
   if (k == kAuto)
-    p.kernel = A.has_csort ? kCsort : ((A.n_ssr > 0) ? kCsr3 : kStream);
+    p.kernel = A.has_csort ? kCsort : (tasks ? kCsr3 : kStream);
   else
     p.kernel = (int)k;
-  if (p.kernel == kCsort && !A.has_csort) p.kernel = (A.n_ssr > 0) ? kCsr3 : kStream;
-  if (p.kernel == kCsr3 && A.n_ssr <= 0) p.kernel = kStream;
+  if (p.kernel == kCsort && !A.has_csort) p.kernel = tasks ? kCsr3 : kStream;
+  if (p.kernel == kCsr3 && !tasks) p.kernel = kStream;
   const int forced_u = (int)((flags >> 16) & 0x1Fu);  // HSPMV_U(u)
   switch (p.kernel) {
     case kCsort:  // the workgroup shape is fixed; the host tables hold the rest

@@ -88,6 +88,24 @@ def build(cfg):
             return A, None, "C3 alt: honeycomb 4280^2 RCM (18.3M rows, 54.9M nnz) CSR fp64"
         maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "volta"))
         return A, maps, "C3 alt: honeycomb 4280^2 RCM CSR-3 fp64 (volta grouping)"
+    if cfg.startswith("d") and cfg[1:].isdigit():  # mid/high density band: d<k> nnz per row
+        k = int(cfg[1:])
+        m = max(50_000_000 // k, 1000)
+        A = gen.banded(m, per_row=k, half=k, seed=21, chunk=max((1 << 22) // (2 * k + 1), 256))
+        return A, None, f"density band: {m} rows x {k} nnz within +-{k}, CSR fp64 (~50M nnz)"
+    if cfg == "mix":  # SuiteSparse-like mixed row lengths (Pareto, 8..4000), band +-4000
+        import scipy.sparse as sp
+        rng = np.random.default_rng(31)
+        m = 1_000_000
+        lens = np.minimum((8 * (rng.pareto(1.2, m) + 1)).astype(np.int64), 4000)
+        rows = np.repeat(np.arange(m, dtype=np.int64), lens)
+        ci = np.clip(rows + rng.integers(-4000, 4001, rows.shape[0]), 0, m - 1)
+        S = sp.csr_matrix((rng.uniform(-1, 1, ci.shape[0]), (rows, ci)), shape=(m, m))
+        S.sum_duplicates()
+        S.sort_indices()
+        A = hspmv.CsrMatrix.from_scipy(S, np.float64)
+        return A, None, (f"mixed rows: {m} rows, Pareto lengths 8..4000 (mean {A.nnz / m:.0f}), "
+                         "band +-4000, CSR fp64")
     if cfg == "c5":
         A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32)
         maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))

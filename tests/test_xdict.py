@@ -52,7 +52,25 @@ def block_rows(A, maps, kernel):
     if start < A.m or not starts:
         starts.append(start)
     starts.append(A.m)
+    starts = cap_tasks(A, starts)
     return np.array(starts[::4] + ([A.m] if (len(starts) - 1) % 4 else []))
+
+
+def cap_tasks(A, starts, budget=2048, long_t=4096):
+    """Tasks over the nonzero budget are cut at rows (in-kernel rows only:
+    split rows count 0), hspmv_api.cpp cap_task_nnz."""
+    lens = np.diff(A.row_ptr)
+    lens = np.where(lens > long_t, 0, lens)
+    out = []
+    for a, b in zip(starts[:-1], starts[1:]):
+        out.append(a)
+        acc = 0
+        for r in range(a, b):
+            if r > out[-1] and acc + lens[r] > budget:
+                out.append(r)
+                acc = 0
+            acc += lens[r]
+    return out + [starts[-1]]
 
 
 def check_plan(A, plan, bounds, split=True, cap=None):
