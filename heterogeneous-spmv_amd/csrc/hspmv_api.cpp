@@ -718,32 +718,33 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
 // row's columns to be non-decreasing slab by slab (sorted rows; checked).
 // HSPMV_XSLABS=0 disables, =B forces B slabs; HSPMV_XSLAB_BYTES moves the
 // slab size.
-// Irregular gathers: the median 64-row group gathers over more than an
-// XCD's 4 MiB L2 of x (random / power-law columns), so nearly every gather
-// of the row kernels is its own L2 request.
+// Irregular gathers: one gather instruction of the row kernels covers 64
+// consecutive nonzeros; when those fall on mostly distinct x cache lines
+// (random / power-law / wide-band columns) every lane is its own L2 request
+// and the row kernels run at the L2 request rate, whatever x's span.  Mean
+// distinct 128-byte lines per 64 consecutive nonzeros, sampled over <= 16 K
+// such runs: C2 5.3, C3 11.1, honeycomb 4.6, C4 5.0, d48/d512 banded 6.9 /
+// 8.9 -- against C5 62.1 and the mixed-length +-4000 band 49.5 (row kernel
+// 210 us, csort 130 us; profiles/r02z5_ab_mix.jsonl).  Irregular: >= 32.
+// (The earlier test -- the median 64-row group spans more than 4 MiB of x
+// -- missed the band.)
 bool irregular_gathers(const int32_t *rp, const int32_t *col, int64_t m, double sv) {
-  const int64_t ng = (m + 63) / 64;
-  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, m / 65536));
-  std::vector<int64_t> wide((size_t)nt, 0), nonempty((size_t)nt, 0);
-  std::vector<std::thread> th;
-  for (int t = 0; t < nt; ++t)
-    th.emplace_back([&, t]() {
-      for (int64_t g = ng * t / nt; g < ng * (t + 1) / nt; ++g) {
-        const int64_t k0 = rp[64 * g], k1 = rp[std::min(m, 64 * g + 64)];
-        if (k1 <= k0) continue;
-        int32_t lo = col[k0], hi = col[k0];
-        for (int64_t k = k0 + 1; k < k1; ++k) {
-          lo = std::min(lo, col[k]);
-          hi = std::max(hi, col[k]);
-        }
-        ++nonempty[(size_t)t];
-        if ((double)(hi - lo + 1) * sv > 4.0 * 1024 * 1024) ++wide[(size_t)t];
-      }
-    });
-  for (auto &x : th) x.join();
-  int64_t nw = 0, ne = 0;
-  for (int t = 0; t < nt; ++t) { nw += wide[(size_t)t]; ne += nonempty[(size_t)t]; }
-  return 2 * nw > ne;
+  const int64_t nnz = rp[m];
+  const int64_t runs = nnz / 64;
+  if (runs == 0) return false;
+  const int64_t step = std::max<int64_t>(1, runs / 16384);
+  const int32_t per_line = (int32_t)(128.0 / sv);
+  int64_t lines = 0, sampled = 0;
+  int32_t c[64];
+  for (int64_t r = 0; r < runs; r += step) {
+    for (int j = 0; j < 64; ++j) c[j] = col[r * 64 + j] / per_line;
+    std::sort(c, c + 64);
+    int d = 1;
+    for (int j = 1; j < 64; ++j) d += c[j] != c[j - 1];
+    lines += d;
+    ++sampled;
+  }
+  return lines >= 32 * sampled;
 }
 
 constexpr double kSlabBytes = 2.0 * 1024 * 1024;

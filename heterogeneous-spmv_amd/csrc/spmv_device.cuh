@@ -41,7 +41,10 @@ __device__ __forceinline__ unsigned long long diag_stamp() {
 #endif
 
 constexpr int kWave = 64;
-constexpr int kSerialMax = 32;  // longest row summed serially by one lane
+#ifndef HSPMV_SERIAL_MAX
+#define HSPMV_SERIAL_MAX 32
+#endif
+constexpr int kSerialMax = HSPMV_SERIAL_MAX;  // longest row summed serially by one lane
 constexpr int kNumXcd = 8;
 
 template <bool NT, typename T>
