@@ -41,6 +41,9 @@ __device__ __forceinline__ unsigned long long diag_stamp() {
 #endif
 
 constexpr int kWave = 64;
+#ifndef HSPMV_COOP_GROUPS
+#define HSPMV_COOP_GROUPS 1
+#endif
 #ifndef HSPMV_SERIAL_MAX
 #define HSPMV_SERIAL_MAX 32
 #endif
@@ -90,6 +93,29 @@ __device__ __forceinline__ T dpp_move(T v) {
 // total), returned wave-uniform.  No LDS round trips, unlike __shfl_xor
 // (ds_bpermute): the cooperative rows' reductions are on the critical path
 // of each chunk (mid-density rows, profiles/r02z*).
+// Lane l's value of v, wave-uniform (v_readlane; l wave-uniform).
+template <typename T>
+__device__ __forceinline__ T lane_value(T v, int l) {
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+  }
+}
+
+// Sums of the four 16-lane DPP rows: lane 16 q + 15 holds row q's total.
+template <typename T>
+__device__ __forceinline__ T row16_sum_dpp(T v) {
+  v += dpp_move<0x111, 0xf>(v);
+  v += dpp_move<0x112, 0xf>(v);
+  v += dpp_move<0x114, 0xf>(v);
+  v += dpp_move<0x118, 0xf>(v);
+  return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum_dpp(T v) {
   v += dpp_move<0x111, 0xf>(v);
@@ -98,14 +124,7 @@ __device__ __forceinline__ T wave_sum_dpp(T v) {
   v += dpp_move<0x118, 0xf>(v);
   v += dpp_move<0x142, 0xa>(v);
   v += dpp_move<0x143, 0xc>(v);
-  if constexpr (sizeof(T) == 8) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)b, 63);
-    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 63);
-    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
-  } else {
-    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
-  }
+  return lane_value(v, 63);
 }
 
 // Bijective XCD-aware block order (cdna_hip_programming.md §5 "XCD swizzle
@@ -224,7 +243,7 @@ struct XWin {
 // C forms the products into LDS; then the row sums.  PF (software
 // pipelining): the next chunk's stage A is issued between this chunk's
 // stage B and C, so its latency overlaps the gather and the sums.
-template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD>
+template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD, bool GROUPS>
 __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, int32_t end,
                                           int32_t long_t, const ColSrc &cs,
                                           const T *__restrict__ val,
@@ -349,6 +368,42 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         // only the cooperative rows this chunk touches (rows are contiguous:
         // the others would add nothing), bounds by readlane (scalar)
         unsigned long long cm = coop ? coop & __ballot(end > c && beg <= c + last) : 0ull;
+        // three or more pieces (rows of 33..~100 nonzeros): four at a time,
+        // one 16-lane DPP row each.  CSR3 kernel only -- the tasks that
+        // mid-density CSR matrices run as (hspmv_api.cpp build_tasks): in
+        // the STREAM kernel the extra code cost the honeycomb matrix 4 %
+        // (161 -> 168 us) with no such rows at all (r02z9).  d33 173 ->
+        // 137 us, d48 132 -> 109, d64 103 -> 95 (profiles/r02z8).
+        if (GROUPS && __popcll(cm) >= 3) {
+          const int g = lane >> 4, gl = lane & 15;
+          while (cm) {
+            int rq[4];
+            int32_t lq[4], hq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              rq[q] = -1;
+              lq[q] = 0;
+              hq[q] = 0;
+              if (cm) {  // wave-uniform
+                rq[q] = __ffsll(cm) - 1;
+                cm &= cm - 1;
+                lq[q] = max(__builtin_amdgcn_readlane(beg, rq[q]), c);
+                hq[q] = min(__builtin_amdgcn_readlane(end, rq[q]), c + last + 1);
+              }
+            }
+            const int32_t lo = g == 0 ? lq[0] : (g == 1 ? lq[1] : (g == 2 ? lq[2] : lq[3]));
+            const int32_t hi = g == 0 ? hq[0] : (g == 1 ? hq[1] : (g == 2 ? hq[2] : hq[3]));
+            T s = T(0);
+            for (int32_t k = lo + gl; k < hi; k += 16) s += lds[k - c];
+            s = row16_sum_dpp(s);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (rq[q] >= 0) {  // wave-uniform
+                const T t = lane_value(s, 16 * q + 15);
+                if (lane == rq[q]) acc += t;
+              }
+          }
+        }
         while (cm) {
           const int r = __ffsll(cm) - 1;
           cm &= cm - 1;
@@ -502,7 +557,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
     if (g1 < gend) group_bounds(rp, g1, (int32_t)min<int64_t>(g1 + kWave, gend), lane, nbeg, nend);
     int32_t gbase = 0;
     if constexpr (C16 == 2) gbase = (int32_t)sload_i64(cs.cbase, (uint64_t)(g0 / kWave) * 4u);
-    wave_rows<T, NT, U, PF, C16, XW, XD>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my,
+    wave_rows<T, NT, U, PF, C16, XW, XD, false>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my,
                                          lane, win, y_nt != 0, carry != 0, gbase, ts);
     ts = nullptr;  // trace the first group only
     if (g1 >= gend) break;
@@ -563,7 +618,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     const int32_t g1 = min(g0 + kWave, r1);
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
-    wave_rows<T, NT, U, PF, C16, XW, XD>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
+    wave_rows<T, NT, U, PF, C16, XW, XD, HSPMV_COOP_GROUPS != 0>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
                                          win, y_nt != 0, carry != 0, gbase, ts);
     ts = nullptr;
     beg = nbeg;
