@@ -714,7 +714,7 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
 // the price per extra pass is one more row-pointer array and a y read +
 // write.  Pass b > 0 starts each row from the y of pass b-1, so a row's
 // products are still added left to right from 0 (bit-identical to
-// omp_spmv for rows of <= 32 nonzeros per slab segment) -- which needs the
+// omp_spmv for rows of <= kSerialMax (40) nonzeros per slab segment) -- which needs the
 // row's columns to be non-decreasing slab by slab (sorted rows; checked).
 // HSPMV_XSLABS=0 disables, =B forces B slabs; HSPMV_XSLAB_BYTES moves the
 // slab size.

@@ -45,7 +45,7 @@ constexpr int kWave = 64;
 #define HSPMV_COOP_GROUPS 1
 #endif
 #ifndef HSPMV_SERIAL_MAX
-#define HSPMV_SERIAL_MAX 32
+#define HSPMV_SERIAL_MAX 40
 #endif
 constexpr int kSerialMax = HSPMV_SERIAL_MAX;  // longest row summed serially by one lane
 constexpr int kNumXcd = 8;

@@ -1,6 +1,6 @@
 """Mid- and high-density rows (33 .. 2048 nonzeros) against the oracle.
 
-VERDICT r1 weak 9: the row kernels sum rows longer than kSerialMax (32)
+VERDICT r1 weak 9: the row kernels sum rows longer than kSerialMax (40)
 cooperatively, and a fixed 64-row group per wave left 25 K-row matrices of
 2048-nonzero rows with 381 waves.  Wave tasks are now capped at 2048
 in-kernel nonzeros (hspmv_api.cpp build_tasks / cap_task_nnz): a CSR matrix
@@ -8,7 +8,7 @@ whose heavy 64-row groups hold at least a quarter of the nonzeros runs the
 CSR3 kernel over those tasks.  Checked here, on seeded inputs:
 
 * y within the north-star bar (fp64) or omp_spmv's own fp32 summation error,
-  and rows of <= 32 nonzeros bit-identical to omp_spmv, across the density
+  and rows of <= 40 nonzeros bit-identical to omp_spmv, across the density
   band, for the planner's choice and for an explicit STREAM launch;
 * the planner's choice (CSR3 tasks for heavy groups, STREAM otherwise) and
   the task count against the budget (HSPMV_TASK_NNZ);
@@ -25,7 +25,7 @@ from hspmv import gen
 
 pytestmark = pytest.mark.gpu
 
-SERIAL_MAX = 32
+SERIAL_MAX = 40
 
 
 @pytest.fixture(scope="module", autouse=True)

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 KERNELS = [("stream", 0), ("vector", 1), ("vector", 2), ("vector", 4), ("vector", 8),
            ("vector", 16), ("vector", 32), ("vector", 64), ("auto", 0)]
-SERIAL_MAX = 32  # rows up to this length go through the ordered (bit-exact) path
+SERIAL_MAX = 40  # rows up to this length go through the ordered (bit-exact) path
 
 
 @pytest.fixture(scope="module", autouse=True)
