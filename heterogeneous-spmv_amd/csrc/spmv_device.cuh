@@ -11,7 +11,9 @@ namespace hspmv {
 namespace dev {
 
 // Ablation builds only (make diag): 1 = skip the ordered row sums, 2 = skip
-// the x gather (x[col] := 1), 3 = both.  Results are wrong in those builds.
+// the x gather (x[col] := 1), 3 = both; 16 = skip the x-dictionary staging
+// (and its barrier), 32 = the barrier without the staging loads.  Results
+// are wrong in those builds.
 #ifndef HSPMV_DIAG
 #define HSPMV_DIAG 0
 #endif
@@ -471,6 +473,11 @@ template <typename T, int NTH>
 __device__ __forceinline__ void stage_xdict(T *xs, const T *__restrict__ x, const XDict &xd,
                                             int64_t blk, int tid) {
   constexpr int kBatch = 8;
+  if constexpr ((HSPMV_DIAG & 16) != 0) return;  // ablation: no staging, no barrier
+  if constexpr ((HSPMV_DIAG & 32) != 0) {        // ablation: the barrier only
+    __syncthreads();
+    return;
+  }
   const int64_t rr = sload_i64(xd.blk, (uint64_t)blk * 4u);
   const int32_t r0 = (int32_t)rr;
   const int32_t nr = (int32_t)(rr >> 32) - r0 - 1;  // runs (<= 63), then the sentinel
