@@ -46,18 +46,18 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    # each entry: path[@flags][#VAR=VALUE] (flags ORed with --flags; the
-    # environment variable is set while that handle is created)
+    # each entry: path[@flags][#VAR=VALUE[#VAR2=VALUE2...]] (flags ORed with
+    # --flags; the environment variables are set while that handle is created)
     entries, envs = [], []
     for e in a.libs.split(","):
         e, _, env = e.partition("#")
-        envs.append(tuple(env.split("=", 1)) if env else None)
+        envs.append([tuple(kv.split("=", 1)) for kv in env.split("#")] if env else None)
         entries.append((e.split("@")[0], int(e.split("@")[1]) if "@" in e else 0))
     cache = {}
     libs = [cache.setdefault(p, load(p)) for p, _ in entries]
     extra = [f for _, f in entries]
     names = [Path(p).parent.name + "/" + Path(p).name + (f"@{f}" if f else "") +
-             (f"#{v[0]}={v[1]}" if v else "") for (p, f), v in zip(entries, envs)]
+             "".join(f"#{k}={w}" for k, w in (v or [])) for (p, f), v in zip(entries, envs)]
     out = []
     for cfg in a.configs.split(","):
         A, maps, desc = build(cfg)
@@ -65,13 +65,13 @@ def main():
         cs, ms = A.c_struct(), (maps.c_struct() if maps is not None and a.kernel != "stream" else None)
         hs = []
         for L, fx, env in zip(libs, extra, envs):
-            if env:
-                os.environ[env[0]] = env[1]
+            for k, w in env or []:
+                os.environ[k] = w
             h = C.c_void_p()
             rc = L.hspmv_create_on_device(C.byref(h), C.byref(cs), C.byref(ms) if ms else None, 0,
                                           None, _KERNELS[a.kernel] | a.flags | fx)
-            if env:
-                os.environ.pop(env[0], None)
+            for k, _ in env or []:
+                os.environ.pop(k, None)
             assert rc == 0, L.hspmv_last_error()
             assert L.hspmv_set_x(h, x.ctypes.data) == 0
             hs.append(h)
