@@ -96,6 +96,9 @@ struct Shard {
   void *d_partials = nullptr;
   // host copies kept until the plan is built
   std::vector<int32_t> h_rp, h_outer, h_inner, h_tasks;
+  // placement trials (place_shard): SpMV time of each array set, the kept one
+  std::vector<double> place_us;
+  int place_pick = 0;
 };
 
 }  // namespace
@@ -365,6 +368,20 @@ bool csr3_packed() {
   return !(e && !strcmp(e, "ssr"));
 }
 
+// Task cut of the packed CSR-3 plan: 64-row groups aligned to multiples of 64
+// rows (default), or whole super-rows packed up to 64 rows
+// (HSPMV_TASK_FILL=0, pack_csr3_tasks).  The row sums are row-local, so y is
+// the same bit for bit either way; what differs is the y stores: a wave's 64
+// rows are 512 B (fp64) / 256 B (fp32) on cache-line boundaries, where C3's
+// ten-row super-rows gave 60-row tasks whose stores split lines between two
+// waves.  C3 fp64 111.0 -> 101.0 us with cached y stores
+// (profiles/r02ab_ab_c3_tasks.jsonl).  The super-super-rows still bound the
+// shards of the multi-GPU split.
+bool csr3_fill() {
+  const char *e = getenv("HSPMV_TASK_FILL");
+  return !(e && atoi(e) == 0);
+}
+
 void pack_csr3_tasks(const std::vector<int32_t> &in, int32_t m, std::vector<int32_t> &ts) {
   constexpr int32_t kTaskRows = 64;  // one wave's lanes
   ts.clear();
@@ -437,7 +454,11 @@ void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner
   if (!csr3_packed()) return;
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
   const int32_t budget = task_nnz_budget();
-  if (inner) {
+  if (inner && csr3_fill()) {
+    for (int64_t g = 0; g < m; g += 64) ts.push_back((int32_t)g);
+    if (ts.empty()) ts.push_back(0);
+    ts.push_back((int32_t)m);
+  } else if (inner) {
     pack_csr3_tasks(*inner, (int32_t)m, ts);
   } else {
     const unsigned k = flags & 0xFu;
@@ -1415,6 +1436,122 @@ int check_handle(hspmv_handle *h) {
   return HSPMV_OK;
 }
 
+// Mean SpMV time (us) of the shard's current arrays: 2 warm-up launches, then
+// the best of 3 event-timed runs of 5 launches.  < 0 on a launch error.
+double time_shard(Shard &s, int dtype) {
+  for (int i = 0; i < 2; ++i)
+    if (launch_spmv(s.A, s.dp, dtype, s.plan, s.x, s.y, s.stream) != hipSuccess) return -1.0;
+  double best = 1e30;
+  for (int r = 0; r < 3; ++r) {
+    if (hipEventRecord(s.ev0, s.stream) != hipSuccess) return -1.0;
+    for (int i = 0; i < 5; ++i)
+      if (launch_spmv(s.A, s.dp, dtype, s.plan, s.x, s.y, s.stream) != hipSuccess) return -1.0;
+    float ms = 0.0f;
+    if (hipEventRecord(s.ev1, s.stream) != hipSuccess || hipEventSynchronize(s.ev1) != hipSuccess ||
+        hipEventElapsedTime(&ms, s.ev0, s.ev1) != hipSuccess)
+      return -1.0;
+    best = std::min(best, 1000.0 * (double)ms / 5.0);
+  }
+  return best;
+}
+
+// Placement trials.  Where a handle's streamed arrays land in HBM moves the
+// HBM-bound row kernels by up to ~10 %: identical C3 handles created one
+// after another in one process ran 101.0, 105.4 and 110.8 us, each stable
+// over its own rounds (profiles/r02ad_ab_placement.jsonl).  So the shard's
+// streamed arrays -- row pointers, the column stream the kernel reads (16-bit
+// positions/offsets or 32-bit columns), values, x and y -- are copied into
+// trials-1 fresh allocations in turn (all held until the end, so each lands
+// elsewhere), every set is timed over a few SpMVs, and the fastest is kept;
+// the others are freed.  The kernel, its tables and every bit of y are the
+// same for all sets.  Single-GPU handles with owned arrays whose row kernel
+// (STREAM / CSR3) streams from HBM; HSPMV_PLACEMENT=K sets the number of sets
+// (0 or 1 = off); memory for the extra sets must be free, else fewer are
+// tried.  Off by default: with 4 sets per handle no faster placement turned
+// up on C3 (the first set won 8 of 8 handles; the trial sets ran 111-117 us
+// against 109-111) and C4's picks did not carry over to the steady state
+// (49.5 vs 49.4 us without trials; profiles/r02ae_ab_placement_trials.jsonl),
+// so what made some handles fast in r02ad is not the placement of these
+// arrays alone.
+constexpr int kPlacementTrials = 0;
+
+int place_shard(Shard &s, int64_t n, int dtype) {
+  int trials = kPlacementTrials;
+  if (const char *e = getenv("HSPMV_PLACEMENT")) trials = std::max(0, std::min(8, atoi(e)));
+  if (trials <= 1 || (s.plan.kernel != kStream && s.plan.kernel != kCsr3) || s.A.m == 0) return HSPMV_OK;
+  const size_t sv = dtype_size(dtype);
+  const int64_t m = s.A.m, nnz = s.A.nnz;
+  if ((double)nnz * (double)(sv + 4) + (double)m * (double)(sv + 4) + (double)n * (double)sv <=
+      kMallResident)
+    return HSPMV_OK;  // served from the Infinity Cache: placement does not matter
+  struct Arr { void **slot; size_t bytes; };
+  std::vector<Arr> arrs = {{(void **)&s.d_rp, 4 * (size_t)(m + 1)},
+                           {(void **)&s.d_val, sv * (size_t)nnz},
+                           {(void **)&s.d_x, sv * (size_t)n},
+                           {(void **)&s.d_y, sv * (size_t)m}};
+  if (s.A.col16)
+    arrs.push_back({(void **)&s.d_c16, 2 * (size_t)nnz});
+  else
+    arrs.push_back({(void **)&s.d_ci, 4 * (size_t)nnz});
+  size_t set_bytes = 0;
+  for (auto &a : arrs) set_bytes += a.bytes;
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const size_t margin = (size_t)1 << 30;
+  const int fit = free_b > margin ? (int)std::min<size_t>(8, (free_b - margin) / set_bytes) : 0;
+  trials = std::min(trials, 1 + fit);
+  if (trials <= 1) return HSPMV_OK;
+  auto point = [&]() {
+    s.A.row_ptr = s.d_rp;
+    s.A.col_idx = s.d_ci;
+    s.A.val = s.d_val;
+    if (s.A.col16) s.A.col16 = s.d_c16;
+    s.x = s.d_x;
+    s.y = s.d_y;
+  };
+  HIP_TRY(hipMemsetAsync(s.d_x, 0, sv * (size_t)n, s.stream));
+  std::vector<std::vector<void *>> sets(1);
+  for (auto &a : arrs) sets[0].push_back(*a.slot);
+  s.place_us.assign(1, time_shard(s, dtype));
+  if (s.place_us[0] < 0) return set_error(HSPMV_E_HIP, "placement trial: launch failed");
+  int rc = HSPMV_OK;
+  for (int k = 1; k < trials && rc == HSPMV_OK; ++k) {
+    std::vector<void *> set;
+    for (auto &a : arrs) {
+      void *p = nullptr;
+      if (hipMalloc(&p, a.bytes) != hipSuccess) break;
+      set.push_back(p);
+      if (hipMemcpyAsync(p, *a.slot, a.bytes, hipMemcpyDeviceToDevice, s.stream) != hipSuccess) {
+        rc = set_error(HSPMV_E_HIP, "placement trial: copy failed");
+        break;
+      }
+    }
+    if (rc != HSPMV_OK || set.size() != arrs.size()) {  // out of memory or a failed copy: stop
+      (void)hipStreamSynchronize(s.stream);
+      for (void *p : set) (void)hipFree(p);
+      (void)hipGetLastError();
+      break;
+    }
+    for (size_t i = 0; i < arrs.size(); ++i) *arrs[i].slot = set[i];
+    point();
+    const double t = time_shard(s, dtype);
+    sets.push_back(set);
+    s.place_us.push_back(t);
+    if (t < 0) rc = set_error(HSPMV_E_HIP, "placement trial: launch failed");
+  }
+  HIP_TRY(hipStreamSynchronize(s.stream));
+  int pick = 0;
+  for (int k = 1; k < (int)sets.size(); ++k)
+    if (s.place_us[(size_t)k] >= 0 && s.place_us[(size_t)k] < s.place_us[(size_t)pick]) pick = k;
+  for (int k = 0; k < (int)sets.size(); ++k)
+    if (k != pick)
+      for (void *p : sets[(size_t)k]) (void)hipFree(p);
+  for (size_t i = 0; i < arrs.size(); ++i) *arrs[i].slot = sets[(size_t)pick][i];
+  point();
+  s.place_pick = pick;
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1513,6 +1650,10 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
     }
   }
   if ((rc = finish_shard(s, A->dtype, flags, stream))) {
+    free_shard(s, h->borrowed);
+    return rc;
+  }
+  if (!devptrs && (rc = place_shard(s, A->n, A->dtype))) {
     free_shard(s, h->borrowed);
     return rc;
   }
@@ -1913,6 +2054,9 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->csort_parts = s.plan.kernel == kCsort ? s.dp.cs.H : 0;
   out->n_split_rows = s.plan.kernel == kCsort ? s.dp.cs.n_long : out->n_split_rows;
   for (auto &sh : h->shards) out->x_dict_entries += sh.dp.xd_blk ? sh.xd_entries : 0;
+  out->placement_trials = (int32_t)s.place_us.size();
+  out->placement_pick = s.place_pick;
+  for (size_t k = 0; k < s.place_us.size() && k < 8; ++k) out->placement_us[k] = s.place_us[k];
   return HSPMV_OK;
 }
 

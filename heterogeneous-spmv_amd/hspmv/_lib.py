@@ -112,7 +112,9 @@ class Info(C.Structure):
                 ("x_entries", C.c_int64), ("format_bytes", C.c_double), ("col16", C.c_int32),
                 ("wave_tasks", C.c_int32), ("x_windows", C.c_int32), ("x_dict", C.c_int32),
                 ("x_dict_entries", C.c_int64), ("x_slabs", C.c_int32),
-                ("col16_group", C.c_int32), ("csort_parts", C.c_int32)]
+                ("col16_group", C.c_int32), ("csort_parts", C.c_int32),
+                ("placement_trials", C.c_int32), ("placement_pick", C.c_int32),
+                ("placement_us", C.c_double * 8)]
 
 
 _P = C.c_void_p

@@ -416,6 +416,7 @@ class SpMV:
         i = _lib.Info()
         check(lib().hspmv_get_info(self._h, C.byref(i)), "hspmv_get_info")
         d = {k: getattr(i, k) for k, _ in _lib.Info._fields_}
+        d["placement_us"] = [round(v, 3) for v in d["placement_us"][:d["placement_trials"]]]
         d["kernel_name"] = KERNEL_NAMES.get(d["kernel"], "?")
         return d
 

@@ -63,7 +63,7 @@ def main():
         A, maps, desc = build(cfg)
         x = gen.rand_x(A.n, 42).astype(A.val.dtype)
         cs, ms = A.c_struct(), (maps.c_struct() if maps is not None and a.kernel != "stream" else None)
-        hs = []
+        hs, places = [], []
         for L, fx, env in zip(libs, extra, envs):
             for k, w in env or []:
                 os.environ[k] = w
@@ -75,6 +75,10 @@ def main():
             assert rc == 0, L.hspmv_last_error()
             assert L.hspmv_set_x(h, x.ctypes.data) == 0
             hs.append(h)
+            inf = _lib.Info()
+            assert L.hspmv_get_info(h, C.byref(inf)) == 0
+            places.append([round(v, 2) for v in inf.placement_us[:inf.placement_trials]] +
+                          ([f"pick {inf.placement_pick}"] if inf.placement_trials else []))
         ys = []
         for L, h in zip(libs, hs):
             y = np.empty(A.m, dtype=A.val.dtype)
@@ -91,7 +95,7 @@ def main():
             rec = {"config": cfg, "lib": names[i], "kernel": a.kernel,
                    "t_min_us": round(min(t[0] for t in times[i]) * 1e6, 3),
                    "t_med_us": round(float(np.median([t[1] for t in times[i]])) * 1e6, 3),
-                   "y_equal_to_first": same[i]}
+                   "y_equal_to_first": same[i], "placement_us": places[i]}
             out.append(rec)
             print(json.dumps(rec), flush=True)
         for L, h in zip(libs, hs):

@@ -145,6 +145,10 @@ typedef struct {
                           256-nonzero blocks or none                        */
   int32_t csort_parts; /* CSORT: column parts H of the row blocks (0 = the
                           handle does not use the column-sorted kernel)     */
+  int32_t placement_trials; /* array sets timed at creation (0 = none: see
+                               HSPMV_PLACEMENT in hspmv_create_on_device)  */
+  int32_t placement_pick;   /* the set kept (0 = the first allocation)      */
+  double placement_us[8];   /* each set's mean SpMV time at creation, us    */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
@@ -231,7 +235,15 @@ int hspmv_create_sharded(hspmv_handle **h, const hspmv_csr *A,
 
 /* Single-device handle on `device`, launching on `stream` (a hipStream_t;
  * NULL = the library creates one).  This is the entry a one-process-per-GPU
- * caller (torch.distributed, MPI) uses for its row-range shard. */
+ * caller (torch.distributed, MPI) uses for its row-range shard.
+ * Placement trials: for a handle that owns its arrays (no
+ * HSPMV_FLAG_DEVICE_PTRS) and whose STREAM / CSR3 kernel streams from HBM,
+ * the row pointers, column stream, values, x and y are copied into up to
+ * three further allocations, each copy is timed over a few SpMVs and the
+ * fastest placement is kept (the others are freed; y bits do not depend on
+ * it).  Opt-in: environment HSPMV_PLACEMENT=K (K <= 8 sets; default off --
+ * measured no gain); hspmv_info reports the times.  With trials
+ * on, creation launches the kernel. */
 int hspmv_create_on_device(hspmv_handle **h, const hspmv_csr *A,
                            const hspmv_csr3_maps *maps, int device,
                            void *stream, unsigned flags);

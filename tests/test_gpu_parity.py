@@ -98,14 +98,18 @@ def test_golden_csr3_fixtures(manifest):
                 check_fp64(A, x, y)
 
 
-@pytest.mark.parametrize("plan", ["packed", "ssr"])
+@pytest.mark.parametrize("plan", ["aligned", "packed", "ssr"])
 @pytest.mark.parametrize("waves_case", [(7, 8), (20, 10), (64, 4), (1, 1), (400, 2), (2, 100)])
 def test_csr3_map_sizes(waves_case, plan, monkeypatch):
     """Any map granularity (tiny super-rows, one-row super-rows, huge SSRs
     that need several waves and several 64-row groups, super-rows of more
-    than 64 rows) gives the same y, under both CSR-3 task plans."""
+    than 64 rows) gives the same y, under the three CSR-3 task plans
+    (64-row aligned tasks, super-rows packed into tasks, a workgroup per
+    super-super-row)."""
     if plan == "ssr":
         monkeypatch.setenv("HSPMV_CSR3_PLAN", "ssr")
+    if plan == "packed":
+        monkeypatch.setenv("HSPMV_TASK_FILL", "0")
     ssrs, srs = waves_case
     # the banded matrix's tasks take the LDS x-window path (span <= 256 columns)
     for A in (gen.laplace2d(300, 200), gen.powerlaw(30000, seed=11, dtype=np.float64),
@@ -114,7 +118,7 @@ def test_csr3_map_sizes(waves_case, plan, monkeypatch):
         x = gen.rand_x(A.n, 5)
         y, info = gpu_spmv(A, x, maps)
         assert info["kernel_name"] == "csr3"
-        if plan == "packed":  # whole super-rows per task, <= 64 rows each
+        if plan != "ssr":  # aligned 64-row groups, or whole super-rows per task (<= 64 rows)
             sr_rows = np.diff(maps.inner)
             lower = int(np.ceil(A.m / 64))
             # plus the cuts of tasks over the 2048-nonzero budget (two

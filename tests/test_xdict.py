@@ -32,11 +32,15 @@ def _long_rows():
     return hspmv.CsrMatrix(600, 20000, rp, ci, rng.uniform(-1, 1, rp[-1]))
 
 
-def block_rows(A, maps, kernel):
+def block_rows(A, maps, kernel, fill=True):
     """Workgroup row ranges the planner uses (STREAM: 256 rows; CSR3: four
-    packed <= 64-row tasks, whole super-rows)."""
+    tasks, 64-row aligned groups by default, or with HSPMV_TASK_FILL=0
+    whole super-rows packed into <= 64-row tasks; both cut at the budget)."""
     if maps is None or kernel == "stream":
         return np.append(np.arange(0, A.m, 256), A.m)
+    if fill:
+        starts = cap_tasks(A, list(range(0, A.m, 64)) + [A.m])
+        return np.array(starts[::4] + ([A.m] if (len(starts) - 1) % 4 else []))
     starts, start = [], 0
     inner = maps.inner
     for sr in range(len(inner) - 1):
@@ -100,8 +104,11 @@ def check_plan(A, plan, bounds, split=True, cap=None):
             assert np.array_equal(staged[pos[k].astype(np.int64)], x[A.col_idx[k]]), (b, r)
 
 
+@pytest.mark.parametrize("fill", [True, False])
 @pytest.mark.parametrize("case", ["lap", "stencil", "banded", "random", "longrows"])
-def test_plan_addresses_every_nonzero(case):
+def test_plan_addresses_every_nonzero(case, fill, monkeypatch):
+    if not fill:
+        monkeypatch.setenv("HSPMV_TASK_FILL", "0")
     A = {"lap": lambda: gen.laplace2d(120, 90),
          "stencil": lambda: gen.stencil27(14),
          "banded": lambda: gen.banded(5000, per_row=10, half=32, seed=5),
@@ -110,7 +117,7 @@ def test_plan_addresses_every_nonzero(case):
     for kernel, maps in [("stream", None), ("csr3", hspmv.build_csr3_maps(A, 7, 8))]:
         plan = hspmv.xdict_plan(A, maps, kernel=kernel, cap_entries=65536)
         assert plan is not None
-        check_plan(A, plan, block_rows(A, maps, kernel))
+        check_plan(A, plan, block_rows(A, maps, kernel, fill))
     if case == "longrows":  # without split rows every row is in the dictionary
         plan = hspmv.xdict_plan(A, None, kernel="stream", cap_entries=65536, split=False)
         check_plan(A, plan, block_rows(A, None, "stream"), split=False)
