@@ -126,11 +126,23 @@ using namespace hspmv;
 
 namespace {
 
+// HSPMV_CONTIG=1 (A/B): physically contiguous device allocations
+// (hipDeviceMallocContiguous; plain hipMalloc when that fails).
+bool contig_alloc() {
+  const char *e = getenv("HSPMV_CONTIG");
+  return e && atoi(e) == 1;
+}
+
 template <typename T>
 int dev_alloc(T **p, size_t bytes, int64_t *acc) {
   *p = nullptr;
   if (bytes == 0) bytes = 16;
-  hipError_t e = hipMalloc((void **)p, bytes);
+  hipError_t e = hipErrorMemoryAllocation;
+  if (contig_alloc()) {
+    e = hipExtMallocWithFlags((void **)p, bytes, hipDeviceMallocContiguous);
+    if (e != hipSuccess) (void)hipGetLastError();
+  }
+  if (e != hipSuccess) e = hipMalloc((void **)p, bytes);
   if (e != hipSuccess)
     return set_error(HSPMV_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
   *acc += (int64_t)bytes;

@@ -25,11 +25,12 @@
 //      CSR-stream scheme (coalesced stream + LDS segmented sums).
 //
 //  * hspmv_csr3<T, NT, U, W>      (HSPMV_KERNEL_CSR3)
-//      CSR-3: one workgroup of W waves per super-super-row (outer map).  The
-//      host planner splits each super-super-row's super-rows (inner map)
-//      into W contiguous, nnz-balanced row ranges -- the multilevel maps
-//      decide where a wave's work starts -- and each wave runs the stream
-//      routine over its range.  Replaces cuSpMV_3 / cuSpMV_3_vec (thread or
+//      CSR-3: wave tasks planned on the host, four per workgroup: 64-row
+//      aligned groups by default (cache-line-aligned y stores), super-rows
+//      packed into <= 64-row tasks (HSPMV_TASK_FILL=0), or one workgroup of
+//      W waves per super-super-row whose super-rows are split W ways by
+//      nonzeros (HSPMV_CSR3_PLAN=ssr); each wave runs the stream routine
+//      over its task (hspmv_api.cpp build_tasks).  Replaces cuSpMV_3 / cuSpMV_3_vec (thread or
 //      sub-warp per row inside (8,12)-thread blocks, csrk.cu:185-319) and
 //      cuSpMV_2 (degenerate outer level).
 //

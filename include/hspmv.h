@@ -158,9 +158,11 @@ typedef struct hspmv_handle hspmv_handle;
 #define HSPMV_KERNEL_VECTOR 1u /* L lanes (sub-wave) per row, shuffle sum  */
 #define HSPMV_KERNEL_STREAM 2u /* wave per 64-row group, LDS-staged,
                                   ordered per-row sums (bit-exact vs CPU)  */
-#define HSPMV_KERNEL_CSR3 3u   /* super-rows packed into <= 64-row wave
-                                  tasks, 4 per workgroup (or one workgroup
-                                  per super-super-row: HSPMV_CSR3_PLAN=ssr) */
+#define HSPMV_KERNEL_CSR3 3u   /* 64-row aligned wave tasks, 4 per
+                                  workgroup (HSPMV_TASK_FILL=0: super-rows
+                                  packed into <= 64-row tasks; or one
+                                  workgroup per super-super-row:
+                                  HSPMV_CSR3_PLAN=ssr)                    */
 #define HSPMV_KERNEL_CSORT 4u  /* column-sorted row blocks: each workgroup
                                   walks its rows' nonzeros in column order,
                                   fp64 LDS row sums (irregular gathers; not
@@ -345,8 +347,8 @@ int hspmv_partition_rows(int64_t m, const int32_t *row_ptr,
  * a row-range shard of a banded matrix -- hspmv_info.x_entries). */
 /* Block x dictionaries (host planner; hspmv_create builds the same tables
  * when it uses them, see hspmv_info.x_dict).  The row kernel's workgroups
- * (STREAM: 256 consecutive rows; CSR3 with maps: four consecutive packed
- * wave tasks) each stage the x entries their rows reference -- runs of
+ * (STREAM: 256 consecutive rows; CSR3 with maps: four consecutive wave
+ * tasks) each stage the x entries their rows reference -- runs of
  * consecutive columns, gaps of <= 8 bridged, <= 63 runs -- in LDS, and every
  * nonzero's column becomes a 16-bit position in that copy.  Outputs:
  * blk[n_blocks+1] record ranges; runs[2*n_records] = {x_start, lds_off} per

@@ -62,3 +62,29 @@ def test_no_torch_or_oracle_symbols_in_product():
     out = subprocess.run(["nm", "-D", str(_lib.LIB_PATH)], capture_output=True, text=True,
                          check=True).stdout
     assert "orc_" not in out and "torch" not in out
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """The ctypes mirrors (hspmv/_lib.py) have the header's sizes and field
+    offsets: a mismatch makes hspmv_get_info / hspmv_run write past the
+    caller's struct (a C program built against an older header crashes the
+    same way -- rebuild the tools after a header change)."""
+    structs = {"hspmv_info": _lib.Info, "hspmv_timing": _lib.Timing}
+    lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "hspmv.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'  printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(_lib.HEADER.parent), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        cname, what, val = line.split()
+        got[(cname, what)] = int(val)
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
