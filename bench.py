@@ -42,6 +42,7 @@ import argparse
 import json
 import math
 import os
+import re
 import subprocess
 import sys
 import time
@@ -159,13 +160,23 @@ def reduce_over_ranks(v: float, world: int, op: str) -> float:
     return float(t.item())
 
 
+def round_order(p: Path):
+    """Sort key of a profile name 'r<round><pass letters>_...': round, then
+    pass (a..z, then aa..zz), then the name."""
+    m = re.match(r"r(\d+)([a-z]*)_", p.name)
+    if not m:
+        return (-1, 0, "", p.name)
+    return (int(m.group(1)), len(m.group(2)), m.group(2), p.name)
+
+
 def load_traffic(workload_key: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary
     (profiles/*_pmc.json, written by heterogeneous-spmv_amd/tools/pmc_summary.py),
     or None when no summary for this workload exists.  The newest file wins
-    (profiles are named per round, r01_ < r02_ ...)."""
+    (profiles are named per round and pass: r01_ < r02_ < r02a < r02z <
+    r02aa ..., by round_order)."""
     best = None
-    for p in sorted((REPO / "profiles").glob("*_pmc.json")):
+    for p in sorted((REPO / "profiles").glob("*_pmc.json"), key=round_order):
         try:
             d = json.loads(p.read_text())
         except Exception:
