@@ -478,6 +478,10 @@ __device__ __forceinline__ void stage_xdict(T *xs, const T *__restrict__ x, cons
     __syncthreads();
     return;
   }
+  // HSPMV_DIAG & 64 / 128 (A/B, results correct): the staging waves at
+  // issue priority 3 / 1 until the barrier, ahead of other blocks' streams
+  if constexpr ((HSPMV_DIAG & 64) != 0) __builtin_amdgcn_s_setprio(3);
+  if constexpr ((HSPMV_DIAG & 128) != 0) __builtin_amdgcn_s_setprio(1);
   const int64_t rr = sload_i64(xd.blk, (uint64_t)blk * 4u);
   const int32_t r0 = (int32_t)rr;
   const int32_t nr = (int32_t)(rr >> 32) - r0 - 1;  // runs (<= 63), then the sentinel
@@ -509,6 +513,7 @@ __device__ __forceinline__ void stage_xdict(T *xs, const T *__restrict__ x, cons
       if (e[j] < total) xs[e[j]] = v[j];
   }
   __syncthreads();
+  if constexpr ((HSPMV_DIAG & (64 | 128)) != 0) __builtin_amdgcn_s_setprio(0);
 }
 
 // STREAM: wave w walks `groups` consecutive 64-row groups starting at row
