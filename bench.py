@@ -16,7 +16,8 @@ Workload (``--config``, default by world size; hspmv.dist.default_config):
   N > 1  c4: BASELINE configs[3], the 2e7-row banded matrix (~200 M nnz)
          row-range partitioned over the N GPUs, nnz-balanced (strong scaling).
   Also: c2 (configs[1], weak scaling: 1000 x 1000 rows per GPU), c3h (the
-  hugebubbles-00000 stand-in), c5 (configs[4], CSR-3 fp32 power-law).
+  hugebubbles-00000 stand-in), c5 (configs[4], CSR-3 fp32 power-law) and c5r
+  (the same matrix RCM-permuted, the reference's input ordering).
 ``--dry-run`` prints the partition plan without touching a GPU.
 
 Extra fields on the line:
@@ -28,12 +29,20 @@ Extra fields on the line:
                every launch (a 512 MiB read)
   comm         RCCL x broadcast / y all-gather / halo-exchange times (N > 1),
                timed separately, and the end-to-end rates they imply
+  csr3_maps_plans  (CSR-3 workloads) the same SpMV under the two maps-driven
+               CSR-3 plans, timed in the same process: "packed" (whole
+               super-rows of the inner map packed into <= 64-row wave tasks)
+               and "ssr" (one workgroup per super-super-row of the outer map,
+               the reference's cuSpMV_3 mapping, csrk.cu:245-319); the
+               headline times config.csr3_plan ("aligned": 64-row tasks)
   scaling_reference  (N = 1) the N > 1 default workload, C4, timed on this
-               one GPU: the same-matrix N = 1 point for the strong-scaling curve
+               one GPU: the same-matrix N = 1 point for the strong-scaling
+               curve, its y checked like the headline's
   cpu_baseline the oracle's OpenMP restatement of spmv-csr's omp_spmv on the
                host cores, on the SAME matrix (rank 0 at N = 1 only, bounded
-               sample), value from TimeMin as run_norm.py records it; beside
-               it reference_f32: the reference's own omp_spmv (spmv-csr/spmv.c,
+               sample), value from TimeMin as run_norm.py records it, on the
+               threads the cgroup CPU quota sustains (min ~ avg); beside it
+               reference_f32: the reference's own omp_spmv (spmv-csr/spmv.c,
                built unmodified into oracle/_ref) on the fp32 copy
 """
 from __future__ import annotations
@@ -69,7 +78,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="auto", choices=["auto", "c2", "c3", "c3h", "c4", "c5"],
+    ap.add_argument("--config", default="auto", choices=["auto", "c2", "c3", "c3h", "c4", "c5", "c5r"],
                     help="auto: c3 at N = 1, c4 at N > 1")
     ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "vector", "csr3"])
     ap.add_argument("--lanes", type=int, default=0)
@@ -218,18 +227,24 @@ def host_cpu_info() -> dict:
 def cpu_baseline(A, x, budget_s: float):
     """The oracle's OpenMP restatement of omp_spmv (spmv-csr/spmv.c:92-114) on
     the same matrix, timed with the reference protocol (5 warm-ups + N timed
-    runs, omp_get_wtime per run; spmv.c:164-185) on this host's cores.  The
-    thread count tried first is the physical core count (lscpu), capped by
-    the CPUs this process may use and the cgroup quota; OMP_NUM_THREADS (the
-    box's CPU share) is tried beside it, and the faster TimeMin is reported.
-    value = 2 nnz / TimeMin (run_norm.py records min/max/avg)."""
+    runs, omp_get_wtime per run; spmv.c:164-185) on this host's cores.
+    value = 2 nnz / TimeMin (run_norm.py records min/max/avg).
+
+    Threads: the reported leg runs on the threads the box can SUSTAIN -- the
+    physical cores (lscpu) capped by this process's CPUs and by the cgroup
+    CPU quota (cpu.max).  More threads than the quota reach a fast TimeMin in
+    a burst but are throttled on average (r02: 128 threads under a 16-CPU
+    quota, TimeAvg 20x TimeMin, a baseline that doubled between runs); such
+    candidates are timed too and listed in threads_tried as bursts, never
+    reported as value."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
     hw = host_cpu_info()
     phys = hw["physical_cores"] or hw["affinity_cpus"]
-    cand = {max(1, min(phys, hw["affinity_cpus"]))}
-    if hw["cgroup_cpu_quota"]:
-        cand.add(max(1, min(phys, hw["affinity_cpus"], int(math.ceil(hw["cgroup_cpu_quota"])))))
+    avail = max(1, min(phys, hw["affinity_cpus"]))
+    quota = hw["cgroup_cpu_quota"]
+    sustained = max(1, min(avail, int(math.floor(quota)))) if quota else avail
+    cand = {sustained, avail}
     env_t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     if env_t > 0:
         cand.add(min(env_t, hw["affinity_cpus"]))
@@ -238,8 +253,13 @@ def cpu_baseline(A, x, budget_s: float):
         oracle.set_schedule("static", t)
         tmin, tmax, tavg, used = oracle.time_spmv(A.row_ptr, A.col_idx, A.val, x, warmup=5, runs=20)
         tried[int(used)] = {"time_min_s": tmin, "time_avg_s": tavg,
-                            "gflops_from_min": round(2.0 * A.nnz / tmin * 1e-9, 3)}
-    threads = min(tried, key=lambda t: tried[t]["time_min_s"])
+                            "avg_over_min": round(tavg / tmin, 3),
+                            "gflops_from_min": round(2.0 * A.nnz / tmin * 1e-9, 3),
+                            "within_quota": bool(not quota or used <= quota),
+                            "note": ("reported leg" if used == sustained else
+                                     "burst: above the cgroup CPU quota, throttled on average"
+                                     if quota and used > quota else "not reported")}
+    threads = sustained
     per = max(tried[threads]["time_avg_s"], 1e-6)
     runs = int(max(20, min(20000, 0.5 * budget_s / per)))
     res = {}
@@ -251,11 +271,16 @@ def cpu_baseline(A, x, budget_s: float):
     dt = "fp64" if A.val.dtype == np.float64 else "fp32"
     return {"value": round(2.0 * A.nnz / tmin * 1e-9, 3), "unit": "GFLOP/s", "cores": int(used),
             "kind": "port",
+            "cores_note": (f"{int(used)} OpenMP threads = the sustained CPU share: "
+                           f"{phys} physical cores, {hw['affinity_cpus']} CPUs in the affinity "
+                           f"mask, cgroup quota {quota if quota else 'none'} CPUs"),
+            "cgroup_cpu_quota": quota,
             "sample": (f"the same matrix as the GPU line (m={A.m}, nnz={A.nnz}, {dt}, CSR), "
                        f"omp_spmv restatement (oracle/spmv_oracle.c), OMP_SCHEDULE=static, "
                        f"{int(used)} threads, 5 warm-ups + {runs} timed runs "
                        f"(spmv-csr/spmv.c:164-185 protocol), value = 2 nnz / TimeMin"),
             "time_min_s": tmin, "time_avg_s": tavg, "time_max_s": tmax,
+            "avg_over_min": round(tavg / tmin, 3),
             "gflops_from_avg": round(2.0 * A.nnz / tavg * 1e-9, 3),
             "host": hw, "threads_tried": tried,
             "guided": {"gflops": round(2.0 * A.nnz / g[0] * 1e-9, 3),
@@ -293,6 +318,7 @@ def reference_cpu(A, x, threads: int, budget_s: float):
     tmin, tavg = min(ts), sum(ts) / len(ts)
     return {"kind": "reference", "dtype": "f32", "cores": threads,
             "value": round(2.0 * A.nnz / tmin * 1e-9, 3), "unit": "GFLOP/s",
+            "avg_over_min": round(tavg / tmin, 3),
             "gflops_from_avg": round(2.0 * A.nnz / tavg * 1e-9, 3),
             "time_min_s": tmin, "time_avg_s": tavg, "time_max_s": max(ts), "runs": len(ts),
             "sample": (f"the reference's omp_spmv (oracle/_ref, built from spmv-csr/spmv.c) on the "
@@ -333,13 +359,56 @@ def scaling_reference(args, stream):
     ev_s = ev0.elapsed_time(ev1) * 1e-3 / steps
     info = op.info
     op.close()
+    # the same property check as the headline's y (no oracle in the bench)
+    ok, rel = hdist.checksum_ok(A, x.cpu().numpy(), y.cpu().numpy())
     return {"config": f"{cfg}: {sh.name}", "n_gpus": 1, "m": sh.m_global, "nnz": sh.nnz_global,
+            "check": {"pass": bool(ok), "checksum_rel": rel},
             "value": round(2.0 * sh.nnz_global / step_s * 1e-9, 3), "unit": "GFLOP/s",
             "ms_per_step": round(step_s * 1e3, 6), "steps": steps,
             "launch_us_events": round(ev_s * 1e6, 3), "kernel": info["kernel_name"],
             "frac": round(info["alg_bytes"] / ev_s * 1e-9 / HBM_PEAK_GBS, 4),
             "note": ("the N > 1 default workload on this one GPU: an N-GPU run of it "
                      "(bench.py --gpus N) over N x this value is its strong-scaling efficiency")}
+
+
+def csr3_maps_plans(args, A, maps, x, y_ref, stream, device):
+    """The same CSR-3 SpMV under the two maps-driven plans (hspmv_options
+    csr3_plan), in this process, with the headline's protocol: "packed"
+    packs whole super-rows of the inner map into <= 64-row wave tasks;
+    "ssr" gives each super-super-row of the outer map one workgroup, its
+    super-rows split over the waves by nonzeros -- the reference's cuSpMV_3
+    mapping (csrk.cu:245-319, launched spmv-auto-mi100.cu:200-236).  The row
+    sums are row-local, so y must equal the headline's bit for bit."""
+    import torch
+
+    import hspmv
+    out = {}
+    for plan in ("packed", "ssr"):
+        op = hspmv.SpMV(A, maps, device=device, stream=stream.cuda_stream,
+                        options={"csr3_plan": plan})
+        info = op.info
+        y = torch.empty_like(y_ref)
+        op.bind_x_device(x.data_ptr())
+        op.bind_y_device(y.data_ptr())
+        for _ in range(args.warmup):
+            op.spmv()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for _ in range(args.steps):
+            op.spmv()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
+        out[plan] = {"launch_us_events": round(s * 1e6, 3),
+                     "gflops": round(2.0 * A.nnz / s * 1e-9, 3),
+                     "frac": round(info["alg_bytes"] / s * 1e-9 / HBM_PEAK_GBS, 4),
+                     "kernel": info["kernel_name"], "wave_tasks": info["wave_tasks"],
+                     "waves_per_block": info["waves_per_block"], "blocks": info["blocks"],
+                     "x_dict": info["x_dict"], "csr3_plan": info["csr3_plan"],
+                     "y_bitwise_equal_to_headline": bool(torch.equal(y, y_ref))}
+        op.close()
+    return out
 
 
 # ------------------------------------------------------------------ main
@@ -463,9 +532,17 @@ def main():
     workload_key = f"{cfg}-w{world}-r0-{info['kernel_name']}"
     traffic = load_traffic(workload_key) if rank == 0 else None
 
+    plans = None
+    if maps is not None and info["kernel_name"] == "csr3":
+        plans = csr3_maps_plans(args, A, maps, x, y, stream, local)
+        ok_all = ok_all and reduce_over_ranks(
+            1.0 if all(p["y_bitwise_equal_to_headline"] for p in plans.values()) else 0.0,
+            world, "sum") == world
+
     sref = None
     if world == 1 and cfg != hdist.default_config(2) and not args.no_scaling_ref:
         sref = scaling_reference(args, stream)
+        ok_all = ok_all and sref["check"]["pass"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -500,6 +577,8 @@ def main():
                        "csr3_maps": ({"n_ssr": maps.n_ssr, "n_sr": maps.n_sr} if maps is not None
                                      else None),
                        "kernel": info["kernel_name"], "chunk_u": info["chunk_u"],
+                       "csr3_plan": {0: None, 1: "aligned", 2: "packed", 3: "ssr"}[info["csr3_plan"]],
+                       "deterministic": bool(info["deterministic"]),
                        "xcd_chunk": info["xcd_remap"],
                        "x_dict": info["x_dict"], "x_windows": info["x_windows"],
                        "x_slabs": info["x_slabs"], "col16": info["col16"],
@@ -537,6 +616,7 @@ def main():
                      "iterative_gflops": (round(flops_step / (step_s + halo_ms * 1e-3) * 1e-9, 3)
                                           if halo_ms is not None else round(gflops, 3))},
             "check": {"pass": bool(ok_all), "checksum_rel": rel},
+            "csr3_maps_plans": plans,
             "scaling_reference": sref,
             "cpu_baseline": cpu,
         }

@@ -19,6 +19,10 @@
 //   --x ones|rand:SEED  input vector (default ones, as the reference)
 //   --kernel auto|stream|vector[:L]|csr3|csort
 //   --nt                non-temporal loads of the matrix streams
+//   --plan aligned|packed|ssr   CSR-3 wave-task plan (hspmv_options.csr3_plan;
+//                       ssr = one workgroup per super-super-row, the
+//                       reference's cuSpMV_3 mapping)
+//   --deterministic     only kernels whose y is bit-identical run to run
 //   --dump-y PATH       write y as raw binary (dtype) for external checks
 //   --no-check          skip the serial CPU check
 #pragma once
@@ -43,6 +47,8 @@ struct Options {
   unsigned kernel = HSPMV_KERNEL_AUTO;
   unsigned lanes = 0;
   bool nt = false;
+  int plan = HSPMV_CSR3_PLAN_AUTO;
+  bool deterministic = false;
   bool check = true;
   std::string dump_y;
   std::string params = "mi355x";
@@ -90,6 +96,14 @@ inline bool parse_options(int argc, char **argv, int first, Options &o) {
       } else { fprintf(stderr, "bad --kernel %s\n", v); return false; }
     } else if (a == "--nt") {
       o.nt = true;
+    } else if (a == "--plan") {
+      const char *v = need("--plan"); if (!v) return false;
+      if (!strcmp(v, "aligned")) o.plan = HSPMV_CSR3_PLAN_ALIGNED;
+      else if (!strcmp(v, "packed")) o.plan = HSPMV_CSR3_PLAN_PACKED;
+      else if (!strcmp(v, "ssr")) o.plan = HSPMV_CSR3_PLAN_SSR;
+      else { fprintf(stderr, "bad --plan %s\n", v); return false; }
+    } else if (a == "--deterministic") {
+      o.deterministic = true;
     } else if (a == "--no-check") {
       o.check = false;
     } else if (a == "--dump-y") {
@@ -174,8 +188,21 @@ inline int run_and_report(const hspmv_csr_buf &A, const hspmv_csr3_buf *maps, in
   hspmv_csr3_maps mv = {0, 0, nullptr, nullptr};
   if (maps && maps->n_ssr > 0) mv = {maps->n_ssr, maps->n_sr, maps->outer, maps->inner};
   hspmv_handle *h = nullptr;
-  if (hspmv_create(&h, &view, mv.n_ssr > 0 ? &mv : nullptr, o.gpus, flags_of(o)) != HSPMV_OK)
-    return die("hspmv_create");
+  int ndev = 0;
+  if (hspmv_device_count(&ndev) != HSPMV_OK) return die("hspmv_device_count");
+  const int gpus = o.gpus > 0 ? o.gpus : ndev;
+  std::vector<int> devs((size_t)(gpus > 0 ? gpus : 1));
+  for (size_t p = 0; p < devs.size(); ++p) devs[p] = (int)p;
+  hspmv_options opt;
+  memset(&opt, 0, sizeof(opt));
+  opt.struct_size = sizeof(opt);
+  opt.flags = flags_of(o);
+  opt.devices = gpus > 1 ? devs.data() : nullptr;  // row-range shards over RCCL
+  opt.n_devices = gpus > 1 ? gpus : 0;
+  opt.csr3_plan = o.plan;
+  opt.deterministic = o.deterministic ? 1 : 0;
+  if (hspmv_create_ex(&h, &view, mv.n_ssr > 0 ? &mv : nullptr, &opt) != HSPMV_OK)
+    return die("hspmv_create_ex");
   std::vector<double> x64;
   fill_x(o, A.n, x64);
   if (perm) {
@@ -206,9 +233,11 @@ inline int run_and_report(const hspmv_csr_buf &A, const hspmv_csr3_buf *maps, in
   printf("KernelGBps: %lg\n", t.gbps_alg);
   printf("NumGPUs: %d\n", t.num_gpus);
   static const char *kname[] = {"auto", "vector", "stream", "csr3", "csort"};
-  printf("Kernel: %s lanes=%d waves_per_block=%d blocks=%lld\n",
+  static const char *pname[] = {"-", "aligned", "packed", "ssr"};
+  printf("Kernel: %s lanes=%d waves_per_block=%d blocks=%lld plan=%s deterministic=%d\n",
          kname[(info.kernel >= 0 && info.kernel <= 4) ? info.kernel : 0], info.lanes,
-         info.waves_per_block, (long long)info.blocks);
+         info.waves_per_block, (long long)info.blocks,
+         pname[(info.csr3_plan >= 0 && info.csr3_plan <= 3) ? info.csr3_plan : 0], info.deterministic);
   const size_t sv = A.dtype == HSPMV_F64 ? 8 : 4;
   std::vector<char> y(sv * (size_t)(A.m ? A.m : 1));
   if (hspmv_get_y(h, y.data()) != HSPMV_OK) return die("hspmv_get_y");

@@ -39,6 +39,7 @@ namespace {
 
 constexpr int kWave = 64;
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <bool NT, typename P>
 __device__ __forceinline__ P ld(const P *p) {
@@ -52,33 +53,73 @@ __device__ __forceinline__ int32_t wave_uniform(int32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
-// Loads chunk c's U entries per lane (idx, value).
-template <typename T, int U, bool NT>
+// Loads chunk c's U entries per lane (idx, value): entry u of the lane is
+// the chunk's sorted entry u*64 + lane.  WIDE: 16-byte loads over a layout
+// interleaved on the host (build_csort) so that one load brings the lane
+// two (fp32 records, fp64 values) or four (fp64 indices) of its entries;
+// the entry -> (u, lane) mapping, and so every gather, is unchanged.
+template <typename T, int U, bool NT, bool WIDE>
 __device__ __forceinline__ void load_entries(const void *__restrict__ ent, const T *__restrict__ val,
                                              int32_t c, int lane, uint32_t (&ix)[U], T (&vv)[U]) {
-  const int64_t k0 = (int64_t)c * (kWave * U) + lane;
+  const int64_t k0 = (int64_t)c * (kWave * U);
+  if constexpr (WIDE) {
+    if constexpr (sizeof(T) == 4) {  // records of entries u*64 + lane, (u+1)*64 + lane side by side
+      const u32x4 *p = reinterpret_cast<const u32x4 *>(reinterpret_cast<const u32x2 *>(ent) + k0) + lane;
+#pragma unroll
+      for (int u = 0; u < U; u += 2) {
+        const u32x4 r = ld<NT>(p + (u / 2) * kWave);
+        ix[u] = r.x;
+        vv[u] = __uint_as_float(r.y);
+        ix[u + 1] = r.z;
+        vv[u + 1] = __uint_as_float(r.w);
+      }
+    } else {
+      static_assert(U % 4 == 0, "fp64 wide entries: U multiple of 4");
+      const u32x4 *pi = reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint32_t *>(ent) + k0) + lane;
+#pragma unroll
+      for (int u = 0; u < U; u += 4) {
+        const u32x4 r = ld<NT>(pi + (u / 4) * kWave);
+        ix[u] = r.x;
+        ix[u + 1] = r.y;
+        ix[u + 2] = r.z;
+        ix[u + 3] = r.w;
+      }
+      typedef double f64x2 __attribute__((ext_vector_type(2)));
+      const f64x2 *pv = reinterpret_cast<const f64x2 *>(reinterpret_cast<const double *>(val) + k0) + lane;
+#pragma unroll
+      for (int u = 0; u < U; u += 2) {
+        const f64x2 r = ld<NT>(pv + (u / 2) * kWave);
+        vv[u] = r.x;
+        vv[u + 1] = r.y;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
+    const int64_t k = k0 + lane + u * kWave;
     if constexpr (sizeof(T) == 4) {
-      const u32x2 p = ld<NT>(reinterpret_cast<const u32x2 *>(ent) + k0 + u * kWave);
+      const u32x2 p = ld<NT>(reinterpret_cast<const u32x2 *>(ent) + k);
       ix[u] = p.x;
       vv[u] = __uint_as_float(p.y);
     } else {
-      ix[u] = ld<NT>(reinterpret_cast<const uint32_t *>(ent) + k0 + u * kWave);
-      vv[u] = ld<NT>(val + k0 + u * kWave);
+      ix[u] = ld<NT>(reinterpret_cast<const uint32_t *>(ent) + k);
+      vv[u] = ld<NT>(val + k);
     }
   }
 }
 
-template <typename T, int U, bool NT, bool PF>
+// S: the LDS row-slot / partial-sum type (double; float only for fp32 data,
+// an A/B variant with half the LDS per row).
+template <typename T, typename S, int U, bool NT, bool PF, bool WIDE>
 __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     int32_t H, int64_t m, int32_t direct, const int32_t *__restrict__ blk_c,
     const int32_t *__restrict__ blk_r, const int32_t *__restrict__ blk_v,
     const int32_t *__restrict__ vslice, const int32_t *__restrict__ cbase,
     const void *__restrict__ ent, const T *__restrict__ val, const T *__restrict__ x,
-    double *__restrict__ part, double *__restrict__ spart, T *__restrict__ y) {
+    S *__restrict__ part, S *__restrict__ spart, T *__restrict__ y) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double *acc = reinterpret_cast<double *>(smem);
+  S *acc = reinterpret_cast<S *>(smem);
   constexpr int NW = kCsortThreads / kWave;
   const int b = blockIdx.x;
   const int rb = b / H, h = b - rb * H;
@@ -86,7 +127,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   const int32_t r0 = blk_r[rb], r1 = blk_r[rb + 1];
   const int32_t v0 = blk_v[b], v1 = blk_v[b + 1];
   const int32_t nr = r1 - r0, nv = v1 - v0;
-  for (int32_t i = threadIdx.x; i <= nr + nv; i += kCsortThreads) acc[i] = 0.0;  // + dummy
+  for (int32_t i = threadIdx.x; i <= nr + nv; i += kCsortThreads) acc[i] = S(0);  // + dummy
   __syncthreads();
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
   uint32_t ix[U];
@@ -94,10 +135,10 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   // PF: the next chunk's entries are loaded while this chunk's gathers are
   // in flight (software pipelining across the wave's chunks)
   if constexpr (PF)
-    if (c0 + wid < c1) load_entries<T, U, NT>(ent, val, c0 + wid, lane, ix, vv);
+    if (c0 + wid < c1) load_entries<T, U, NT, WIDE>(ent, val, c0 + wid, lane, ix, vv);
   for (int32_t c = c0 + wid; c < c1; c += NW) {  // wave-uniform
     const int32_t base = wave_uniform(cbase[wave_uniform(c)]);
-    if constexpr (!PF) load_entries<T, U, NT>(ent, val, c, lane, ix, vv);
+    if constexpr (!PF) load_entries<T, U, NT, WIDE>(ent, val, c, lane, ix, vv);
     T xv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) xv[u] = x[base + (int32_t)(ix[u] & 0xffffu)];
@@ -110,16 +151,16 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     }
     if constexpr (PF) {
       __builtin_amdgcn_sched_barrier(0);
-      if (c + NW < c1) load_entries<T, U, NT>(ent, val, c + NW, lane, ix, vv);
+      if (c + NW < c1) load_entries<T, U, NT, WIDE>(ent, val, c + NW, lane, ix, vv);
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      double pr;
-      if constexpr (sizeof(T) == 4)
+      S pr;
+      if constexpr (sizeof(T) == 4 && sizeof(S) == 8)
         pr = (double)vvc[u] * (double)xv[u];  // exact
       else
-        pr = (double)(vvc[u] * xv[u]);  // omp_spmv's rounded product
+        pr = (S)(vvc[u] * xv[u]);  // omp_spmv's rounded product
       atomicAdd(&acc[ixc[u] >> 16], pr);
     }
   }
@@ -128,7 +169,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) y[r0 + i] = (T)acc[i];
     return;
   }
-  double *out = part + (int64_t)h * m + r0;
+  S *out = part + (int64_t)h * m + r0;
   for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) out[i] = acc[i];
   for (int32_t i = threadIdx.x; i < nv; i += kCsortThreads) spart[vslice[v0 + i]] = acc[nr + i];
 }
@@ -136,55 +177,100 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
 // y[r] = part[r] + part[m + r] + ... (parts in order), except long rows:
 // blocks past the row blocks sum each long row's slices (one wave per row,
 // fixed lane assignment and shuffle tree).
-template <typename T>
+// R2: two rows per thread with 16-byte partial loads (m even, so every
+// part's rows stay 16-byte aligned).
+template <typename T, typename S, bool R2>
 __global__ __launch_bounds__(256) void hspmv_csort_finish(
-    int64_t m, int32_t H, int64_t row_blocks, const double *__restrict__ part,
+    int64_t m, int32_t H, int64_t row_blocks, const S *__restrict__ part,
     const uint32_t *__restrict__ long_mask, int32_t n_long, const int32_t *__restrict__ long_row,
-    const int32_t *__restrict__ long_cs, const double *__restrict__ spart, T *__restrict__ y) {
+    const int32_t *__restrict__ long_cs, const S *__restrict__ spart, T *__restrict__ y) {
   if ((int64_t)blockIdx.x < row_blocks) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= m) return;
-    if (long_mask && ((long_mask[r >> 5] >> (r & 31)) & 1u)) return;
-    double s = part[r];
-    for (int32_t h = 1; h < H; ++h) s += part[(int64_t)h * m + r];
-    y[r] = (T)s;
-    return;
+    if constexpr (R2) {
+      typedef S s2 __attribute__((ext_vector_type(2)));
+      typedef T t2 __attribute__((ext_vector_type(2)));
+      const int64_t r = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+      if (r >= m) return;
+      s2 s = *reinterpret_cast<const s2 *>(part + r);
+      for (int32_t h = 1; h < H; ++h) {
+        const s2 q = *reinterpret_cast<const s2 *>(part + (int64_t)h * m + r);
+        s.x += q.x;
+        s.y += q.y;
+      }
+      const uint32_t lm = long_mask ? (long_mask[r >> 5] >> (r & 31)) & 3u : 0u;
+      if (lm == 0u) {
+        t2 o;
+        o.x = (T)s.x;
+        o.y = (T)s.y;
+        *reinterpret_cast<t2 *>(y + r) = o;
+      } else {  // a long row's y comes from its slices
+        if (!(lm & 1u)) y[r] = (T)s.x;
+        if (!(lm & 2u)) y[r + 1] = (T)s.y;
+      }
+      return;
+    } else {
+      const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+      if (r >= m) return;
+      if (long_mask && ((long_mask[r >> 5] >> (r & 31)) & 1u)) return;
+      S s = part[r];
+      for (int32_t h = 1; h < H; ++h) s += part[(int64_t)h * m + r];
+      y[r] = (T)s;
+      return;
+    }
   }
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t j = ((int64_t)blockIdx.x - row_blocks) * 4 + (threadIdx.x >> 6);
   if (j >= n_long) return;
-  double s = 0.0;
+  S s = S(0);
   for (int32_t i = long_cs[j] + lane; i < long_cs[j + 1]; i += kWave) s += spart[i];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
   if (lane == 0) y[long_row[j]] = (T)s;
 }
 
-template <typename T, int U, bool NT>
+template <typename T, typename S, int U, bool NT, bool PF, bool WIDE>
+void launch_csort_main(const DevCsort &c, const T *x, S *part, S *spart, T *y, hipStream_t st) {
+  hipLaunchKernelGGL((hspmv_csort<T, S, U, NT, PF, WIDE>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
+                     (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
+                     c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y);
+}
+
+template <typename T, typename S, int U, bool NT>
 hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
-  if (c.prefetch)
-    hipLaunchKernelGGL((hspmv_csort<T, U, NT, true>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
-                       (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
-                       c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, c.part, c.spart, y);
-  else
-    hipLaunchKernelGGL((hspmv_csort<T, U, NT, false>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
-                       (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
-                       c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, c.part, c.spart, y);
+  S *part = static_cast<S *>(c.part), *spart = static_cast<S *>(c.spart);
+  if constexpr (sizeof(T) == 8 && U % 4 != 0) {
+    if (c.wide) return hipErrorInvalidValue;
+    if (c.prefetch) launch_csort_main<T, S, U, NT, true, false>(c, x, part, spart, y, st);
+    else launch_csort_main<T, S, U, NT, false, false>(c, x, part, spart, y, st);
+  } else {
+    if (c.prefetch) {
+      if (c.wide) launch_csort_main<T, S, U, NT, true, true>(c, x, part, spart, y, st);
+      else launch_csort_main<T, S, U, NT, true, false>(c, x, part, spart, y, st);
+    } else {
+      if (c.wide) launch_csort_main<T, S, U, NT, false, true>(c, x, part, spart, y, st);
+      else launch_csort_main<T, S, U, NT, false, false>(c, x, part, spart, y, st);
+    }
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || c.direct) return e;
-  const int64_t rb = (c.m + 255) / 256;
   const int64_t lb = ((int64_t)c.n_long + 3) / 4;
-  hipLaunchKernelGGL((hspmv_csort_finish<T>), dim3((unsigned)(rb + lb)), dim3(256), 0, st, c.m,
-                     c.H, rb, c.part, c.long_mask, c.n_long, c.long_row, c.long_cs, c.spart, y);
+  if (c.wide && c.m % 2 == 0) {
+    const int64_t rb = (c.m / 2 + 255) / 256;
+    hipLaunchKernelGGL((hspmv_csort_finish<T, S, true>), dim3((unsigned)(rb + lb)), dim3(256), 0, st,
+                       c.m, c.H, rb, part, c.long_mask, c.n_long, c.long_row, c.long_cs, spart, y);
+  } else {
+    const int64_t rb = (c.m + 255) / 256;
+    hipLaunchKernelGGL((hspmv_csort_finish<T, S, false>), dim3((unsigned)(rb + lb)), dim3(256), 0, st,
+                       c.m, c.H, rb, part, c.long_mask, c.n_long, c.long_row, c.long_cs, spart, y);
+  }
   return hipGetLastError();
 }
 
-template <typename T, bool NT>
+template <typename T, typename S, bool NT>
 hipError_t launch_csort_nt(const DevCsort &c, const T *x, T *y, hipStream_t st) {
   switch (c.u) {
-    case 4: return launch_csort_u<T, 4, NT>(c, x, y, st);
-    case 8: return launch_csort_u<T, 8, NT>(c, x, y, st);
-    case 16: return launch_csort_u<T, 16, NT>(c, x, y, st);
+    case 4: return launch_csort_u<T, S, 4, NT>(c, x, y, st);
+    case 8: return launch_csort_u<T, S, 8, NT>(c, x, y, st);
+    case 16: return launch_csort_u<T, S, 16, NT>(c, x, y, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -194,11 +280,18 @@ hipError_t launch_csort_nt(const DevCsort &c, const T *x, T *y, hipStream_t st) 
 hipError_t launch_csort(const DevCsort &c, int dtype, const void *x, void *y, hipStream_t st) {
   if (c.m == 0) return hipSuccess;
   if (c.n_wg <= 0 || c.lds_bytes > kCsortMaxLds) return hipErrorInvalidValue;
-  if (dtype == 1)
-    return c.nontemporal ? launch_csort_nt<double, true>(c, (const double *)x, (double *)y, st)
-                         : launch_csort_nt<double, false>(c, (const double *)x, (double *)y, st);
-  return c.nontemporal ? launch_csort_nt<float, true>(c, (const float *)x, (float *)y, st)
-                       : launch_csort_nt<float, false>(c, (const float *)x, (float *)y, st);
+  if (dtype == 1) {
+    if (c.slot32) return hipErrorInvalidValue;
+    return c.nontemporal ? launch_csort_nt<double, double, true>(c, (const double *)x, (double *)y, st)
+                         : launch_csort_nt<double, double, false>(c, (const double *)x, (double *)y, st);
+  }
+  const float *xf = (const float *)x;
+  float *yf = (float *)y;
+  if (c.slot32)
+    return c.nontemporal ? launch_csort_nt<float, float, true>(c, xf, yf, st)
+                         : launch_csort_nt<float, float, false>(c, xf, yf, st);
+  return c.nontemporal ? launch_csort_nt<float, double, true>(c, xf, yf, st)
+                       : launch_csort_nt<float, double, false>(c, xf, yf, st);
 }
 
 }  // namespace hspmv

@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cmath>
 #include <cstdlib>
 #include <atomic>
@@ -32,13 +33,6 @@ namespace {
     if (_e != hipSuccess)                                                          \
       return set_error(HSPMV_E_HIP, "%s failed: %s (%s:%d)", #expr,                \
                        hipGetErrorString(_e), __FILE__, __LINE__);                 \
-  } while (0)
-
-#define RCCL_TRY(expr)                                                             \
-  do {                                                                             \
-    ncclResult_t _r = (expr);                                                      \
-    if (_r != ncclSuccess)                                                         \
-      return set_error(HSPMV_E_RCCL, "%s failed: %s", #expr, ncclGetErrorString(_r)); \
   } while (0)
 
 // One row-range shard on one GPU.
@@ -99,6 +93,7 @@ struct Shard {
   // placement trials (place_shard): SpMV time of each array set, the kept one
   std::vector<double> place_us;
   int place_pick = 0;
+  Tuning tune;  // the handle's planner choices (hspmv_options)
 };
 
 }  // namespace
@@ -126,12 +121,86 @@ using namespace hspmv;
 
 namespace {
 
-// HSPMV_CONTIG=1 (A/B): physically contiguous device allocations
-// (hipDeviceMallocContiguous; plain hipMalloc when that fails).
-bool contig_alloc() {
-  const char *e = getenv("HSPMV_CONTIG");
-  return e && atoi(e) == 1;
+// Planner options -> Tuning.  Fields past the caller's struct_size read as 0.
+int tuning_from_options(const hspmv_options *o, Tuning *t) {
+  *t = Tuning();
+  if (!o) return HSPMV_OK;
+  if (o->struct_size < offsetof(hspmv_options, csr3_plan))
+    return set_error(HSPMV_E_INVALID, "hspmv_options.struct_size %u too small", o->struct_size);
+  hspmv_options v;
+  memset(&v, 0, sizeof(v));
+  memcpy(&v, o, std::min<size_t>(o->struct_size, sizeof(v)));
+  if (v.csr3_plan < 0 || v.csr3_plan > HSPMV_CSR3_PLAN_SSR)
+    return set_error(HSPMV_E_INVALID, "csr3_plan %d unknown", v.csr3_plan);
+  if ((v.csort_parts && v.csort_parts != 1 && v.csort_parts != 2 && v.csort_parts != 4) ||
+      (v.csort_chunk_u && v.csort_chunk_u != 4 && v.csort_chunk_u != 8 && v.csort_chunk_u != 16) ||
+      (v.stream_waves && v.stream_waves != 1 && v.stream_waves != 2 && v.stream_waves != 4) ||
+      v.task_nnz < 0 || v.x_dict_cap < 0 || v.placement_trials < 0 || v.placement_trials > 8)
+    return set_error(HSPMV_E_INVALID, "hspmv_options: value out of range");
+  if (v.deterministic && (v.flags & 0xFu) == kCsort)
+    return set_error(HSPMV_E_INVALID, "HSPMV_KERNEL_CSORT is not deterministic");
+  t->csr3_plan = v.csr3_plan;
+  t->task_nnz = v.task_nnz;
+  t->x_windows = v.x_windows < 0 ? -1 : 0;
+  t->x_dict = v.x_dict < 0 ? -1 : (v.x_dict > 0 ? 1 : 0);
+  t->x_dict_cap = v.x_dict_cap;
+  t->x_slabs = v.x_slabs < 0 ? -1 : v.x_slabs;
+  t->col16_group = v.col16_group < 0 ? -1 : (v.col16_group > 0 ? 1 : 0);
+  t->csort = v.csort < 0 ? -1 : (v.csort > 0 ? 1 : 0);
+  t->csort_parts = v.csort_parts;
+  t->csort_u = v.csort_chunk_u;
+  t->stream_waves = v.stream_waves;
+  t->deterministic = v.deterministic ? 1 : 0;
+  t->placement_trials = v.placement_trials;
+  return HSPMV_OK;
 }
+
+#ifdef HSPMV_ENV_KNOBS
+// Diagnostic builds only (make diag-env): HSPMV_* environment variables
+// override the options, for the A/B scripts under tools/.
+void tuning_from_env(Tuning *t) {
+  auto geti = [](const char *k, int *v) {
+    if (const char *e = getenv(k)) *v = atoi(e);
+  };
+  if (const char *e = getenv("HSPMV_CSR3_PLAN"))
+    t->csr3_plan = !strcmp(e, "ssr") ? HSPMV_CSR3_PLAN_SSR
+                   : !strcmp(e, "packed") ? HSPMV_CSR3_PLAN_PACKED : HSPMV_CSR3_PLAN_ALIGNED;
+  if (const char *e = getenv("HSPMV_TASK_FILL"))
+    if (atoi(e) == 0) t->csr3_plan = HSPMV_CSR3_PLAN_PACKED;
+  geti("HSPMV_TASK_NNZ", &t->task_nnz);
+  if (const char *e = getenv("HSPMV_XWIN")) t->x_windows = atoi(e) == 0 ? -1 : 0;
+  if (const char *e = getenv("HSPMV_XDICT")) t->x_dict = atoi(e) == 0 ? -1 : 1;
+  geti("HSPMV_XDICT_CAP", &t->x_dict_cap);
+  if (const char *e = getenv("HSPMV_XSLABS")) t->x_slabs = atoi(e) == 0 ? -1 : atoi(e);
+  if (const char *e = getenv("HSPMV_XSLAB_BYTES")) t->xslab_bytes = atof(e);
+  if (const char *e = getenv("HSPMV_COL16G")) t->col16_group = atoi(e) == 0 ? -1 : 1;
+  if (const char *e = getenv("HSPMV_CSORT")) t->csort = atoi(e) == 0 ? -1 : 1;
+  geti("HSPMV_CSORT_H", &t->csort_parts);
+  geti("HSPMV_CSORT_U", &t->csort_u);
+  geti("HSPMV_CSORT_NT", &t->csort_nt);
+  geti("HSPMV_CSORT_PF", &t->csort_pf);
+  geti("HSPMV_CSORT_BPC", &t->csort_blocks_per_cu);
+  geti("HSPMV_CSORT_SLOT32", &t->csort_slot32);
+  geti("HSPMV_CSORT_WIDE", &t->csort_wide);
+  geti("HSPMV_STREAM_W", &t->stream_waves);
+  geti("HSPMV_PLACEMENT", &t->placement_trials);
+  geti("HSPMV_CONTIG", &t->contig);
+  geti("HSPMV_XD_WAVES", &t->xd_waves);
+  geti("HSPMV_PF", &t->pf);
+  geti("HSPMV_YNT", &t->y_nt);
+  geti("HSPMV_NT", &t->nt);
+  geti("HSPMV_DYNLDS", &t->dyn_lds);
+}
+#else
+void tuning_from_env(Tuning *) {}
+#endif
+
+// Tuning.contig (A/B, diagnostic builds): physically contiguous device
+// allocations (hipDeviceMallocContiguous; plain hipMalloc when that fails).
+// Set for the duration of one handle creation (creation is not re-entrant per
+// thread).
+thread_local bool t_contig = false;
+bool contig_alloc() { return t_contig; }
 
 template <typename T>
 int dev_alloc(T **p, size_t bytes, int64_t *acc) {
@@ -286,17 +355,16 @@ int build_col16(Shard &s, const int32_t *col, int64_t nnz, int64_t m, int64_t n,
 // matrices (C2: 15.56 -> 15.12 us in one process, bench 724-732 -> 754
 // GFLOP/s); HBM-resident ones keep build_col16's blocks (C4 53.0 vs 55.4
 // us with group bases, c3h/l4k within 1 %; profiles/r01_ab_col16_group*.jsonl).
-// HSPMV_COL16G=0 disables, =1 uses it whenever it fits.  Split rows (read
+// Tuning.col16_group = -1 disables, 1 uses it whenever it fits.  Split rows (read
 // by the split-row kernels from the 32-bit columns) get offset 0.
 // Row groups: STREAM's 64-row groups (starts == nullptr) or the packed CSR3
 // wave tasks [starts[g], starts[g+1]).
 int build_col16g(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int64_t n, int dtype,
                  unsigned flags, const std::vector<int32_t> *starts, bool *used) {
   *used = false;
-  const char *env = getenv("HSPMV_COL16G");
-  const int mode = env ? atoi(env) : -1;  // -1 auto, 0 off, 1 on whenever it fits
+  const int mode = s.tune.col16_group;  // -1 off, 0 auto, 1 on whenever it fits
   const int64_t nnz = rp[m];
-  if (mode == 0 || (flags & HSPMV_FLAG_NO_COL16) || nnz == 0) return HSPMV_OK;
+  if (mode < 0 || (flags & HSPMV_FLAG_NO_COL16) || nnz == 0) return HSPMV_OK;
   const double sv = (double)dtype_size(dtype);
   const bool forced = (flags & HSPMV_FLAG_COL16) != 0 || mode == 1;
   if (!forced && (double)nnz * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv > kMallResident)
@@ -367,32 +435,28 @@ int build_col16g(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int
 // x windows of the STREAM kernel's 64-row groups: {lo, w} with w = the
 // group's column span when it is at most kXWin entries (its x slice is then
 // staged in LDS and gathered from there), else 0.  Kept only when at least
-// half of the groups qualify (banded matrices); HSPMV_XWIN=0 disables.
+// half of the groups qualify (banded matrices); Tuning.x_windows = -1 disables.
 // CSR-3 task packing (the default CSR-3 plan): the super-rows of the inner
 // map, in order, are packed into wave tasks of at most one 64-row group
 // (the lanes of a wave's ordered sums); a super-row longer than 64 rows is
 // cut at 64-row steps.  Four consecutive tasks form a workgroup, so a
 // super-super-row spans as many waves as its rows need instead of a fixed W
 // per launch (handCoarsen's super-super-rows vary ~10x in rows).
-// HSPMV_CSR3_PLAN=ssr selects the workgroup-per-super-super-row plan.
-bool csr3_packed() {
-  const char *e = getenv("HSPMV_CSR3_PLAN");
-  return !(e && !strcmp(e, "ssr"));
-}
+// Tuning.csr3_plan = HSPMV_CSR3_PLAN_SSR selects the workgroup-per-super-
+// super-row plan.
+bool csr3_packed(const Tuning &t) { return t.csr3_plan != HSPMV_CSR3_PLAN_SSR; }
 
 // Task cut of the packed CSR-3 plan: 64-row groups aligned to multiples of 64
 // rows (default), or whole super-rows packed up to 64 rows
-// (HSPMV_TASK_FILL=0, pack_csr3_tasks).  The row sums are row-local, so y is
+// (Tuning.csr3_plan = HSPMV_CSR3_PLAN_PACKED, pack_csr3_tasks).  The row sums are row-local, so y is
 // the same bit for bit either way; what differs is the y stores: a wave's 64
 // rows are 512 B (fp64) / 256 B (fp32) on cache-line boundaries, where C3's
 // ten-row super-rows gave 60-row tasks whose stores split lines between two
-// waves.  C3 fp64 111.0 -> 101.0 us with cached y stores
-// (profiles/r02ab_ab_c3_tasks.jsonl).  The super-super-rows still bound the
-// shards of the multi-GPU split.
-bool csr3_fill() {
-  const char *e = getenv("HSPMV_TASK_FILL");
-  return !(e && atoi(e) == 0);
-}
+// waves.  C3 fp64 111.0 -> 109.6 us and 110.2 -> 109.4 in two one-process
+// A/Bs of the default configuration (profiles/r02ab_ab_c3_tasks.jsonl,
+// r02ac/).  The super-super-rows still bound the shards of the multi-GPU
+// split.
+bool csr3_fill(const Tuning &t) { return t.csr3_plan != HSPMV_CSR3_PLAN_PACKED; }
 
 void pack_csr3_tasks(const std::vector<int32_t> &in, int32_t m, std::vector<int32_t> &ts) {
   constexpr int32_t kTaskRows = 64;  // one wave's lanes
@@ -424,15 +488,11 @@ void pack_csr3_tasks(const std::vector<int32_t> &in, int32_t m, std::vector<int3
 // rows only: split rows are summed elsewhere), cut at row boundaries: with
 // 64 rows of 512-2048 nonzeros one wave would stream 32-128 K nonzeros and a
 // 25 K-row matrix would fill only 381 waves (d2048: 3.9 ms against 120 us
-// for a wave per row, profiles/r02z2_ab_vector.jsonl).  HSPMV_TASK_NNZ moves
-// the budget.
+// for a wave per row, profiles/r02z2_ab_vector.jsonl).  Tuning.task_nnz
+// moves the budget.
 constexpr int32_t kTaskNnz = 2048;
 
-int32_t task_nnz_budget() {
-  const char *e = getenv("HSPMV_TASK_NNZ");
-  const int v = e ? atoi(e) : 0;
-  return v > 0 ? v : kTaskNnz;
-}
+int32_t task_nnz_budget(const Tuning &t) { return t.task_nnz > 0 ? t.task_nnz : kTaskNnz; }
 
 void cap_task_nnz(const int32_t *rp, int32_t long_t, int32_t budget, std::vector<int32_t> &ts) {
   std::vector<int32_t> out;
@@ -461,12 +521,12 @@ void cap_task_nnz(const int32_t *rp, int32_t long_t, int32_t budget, std::vector
 // with the heavy ones cut -- the CSR3 kernel then runs them (a CSR-2 with
 // one-row super-rows).  Both are capped at the budget.
 void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner, unsigned flags,
-                 std::vector<int32_t> &ts) {
+                 const Tuning &tune, std::vector<int32_t> &ts) {
   ts.clear();
-  if (!csr3_packed()) return;
+  if (!csr3_packed(tune)) return;
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
-  const int32_t budget = task_nnz_budget();
-  if (inner && csr3_fill()) {
+  const int32_t budget = task_nnz_budget(tune);
+  if (inner && csr3_fill(tune)) {
     for (int64_t g = 0; g < m; g += 64) ts.push_back((int32_t)g);
     if (ts.empty()) ts.push_back(0);
     ts.push_back((int32_t)m);
@@ -495,16 +555,15 @@ void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner
 // x windows of row groups [starts[g], starts[g+1]) -- the 64-row groups of
 // STREAM when starts is null, the packed CSR-3 tasks otherwise: {lo, w}
 // when the group's columns span w <= kXWin entries, else {0, 0}.  Empty
-// when fewer than half the groups fit (HSPMV_XWIN=0 disables).  Several
+// when fewer than half the groups fit (Tuning.x_windows = -1 disables).  Several
 // windows per group (C2's Laplacian: three runs around r-1000, r, r+1000)
 // were measured and dropped: 15.6 -> 17.2 us on C2, 210 -> 232 us on a
 // 4000^2 Laplacian (profiles/r01_ab_xwin_multi.jsonl) -- the staging and
 // its registers cost more than gathers that hit L2.
 std::vector<int32_t> xwin_table(const int32_t *rp, const int32_t *col, int64_t m,
-                                const std::vector<int32_t> *starts) {
+                                const std::vector<int32_t> *starts, const Tuning &tune) {
   std::vector<int32_t> tab;
-  if (const char *e = getenv("HSPMV_XWIN"))
-    if (atoi(e) == 0) return tab;
+  if (tune.x_windows < 0) return tab;
   const int64_t ng = starts ? (int64_t)starts->size() - 1 : (m + 63) / 64;
   if (ng <= 0) return tab;
   tab.assign((size_t)(2 * ng), 0);
@@ -548,8 +607,8 @@ std::vector<int32_t> xwin_table(const int32_t *rp, const int32_t *col, int64_t m
 // reference ~1500 distinct x in ~4 runs, against ~6800 nonzeros.
 // Auto: matrices that stream from HBM, whose largest dictionary fits
 // kXdCapBytes of LDS and whose staged entries are <= half the nonzeros;
-// HSPMV_XDICT=0/1 turns it off / on (on: whenever it fits the cap),
-// HSPMV_XDICT_CAP=<bytes> moves the cap.  Splits rows (> kLongRow) keep
+// Tuning.x_dict = -1/1 turns it off / on (on: whenever it fits the cap),
+// Tuning.x_dict_cap (bytes) moves the cap.  Splits rows (> kLongRow) keep
 // their 32-bit columns (split-row kernels).
 constexpr int32_t kXdGap = 8;
 constexpr int32_t kXdMaxRuns = 63;          // run records per block live in one wave's lanes
@@ -666,31 +725,28 @@ bool plan_xdict(const int32_t *rp, const int32_t *col, const std::vector<int32_t
 
 // Workgroup row ranges of the row kernel `kern` (STREAM: 256 rows; CSR3:
 // four packed tasks).
-// Packed CSR3 tasks per dictionary workgroup: 4, or 8 with HSPMV_XD_WAVES=8
-// (512 rows share one dictionary: fewer staged entries per row, half the
-// barriers, twice the LDS per block).
-int xd_task_waves() {
-  const char *e = getenv("HSPMV_XD_WAVES");
-  return (e && atoi(e) == 8) ? 8 : 4;
-}
+// Packed CSR3 tasks per dictionary workgroup: 4, or 8 with Tuning.xd_waves
+// (A/B; 512 rows share one dictionary: fewer staged entries per row, half
+// the barriers, twice the LDS per block).
+int xd_task_waves(const Tuning &t) { return t.xd_waves == 8 ? 8 : 4; }
 
-std::vector<int32_t> xdict_blocks(int kern, int64_t m, const std::vector<int32_t> &tasks) {
+std::vector<int32_t> xdict_blocks(int kern, int64_t m, const std::vector<int32_t> &tasks,
+                                  const Tuning &tune) {
   std::vector<int32_t> bs;
   if (kern == kStream) {
     for (int64_t r = 0; r < m; r += 256) bs.push_back((int32_t)r);
     bs.push_back((int32_t)m);
   } else {
     const int64_t nt = (int64_t)tasks.size() - 1;
-    for (int64_t t = 0; t < nt; t += xd_task_waves()) bs.push_back(tasks[(size_t)t]);
+    for (int64_t t = 0; t < nt; t += xd_task_waves(tune)) bs.push_back(tasks[(size_t)t]);
     bs.push_back(tasks[(size_t)nt]);
   }
   return bs;
 }
 
-int64_t xdict_cap_entries(int dtype) {
-  int64_t cap_bytes = kXdCapBytes;
-  if (const char *e = getenv("HSPMV_XDICT_CAP")) cap_bytes = atoll(e);
-  // <= 64 KiB of LDS (and 16-bit positions) whatever HSPMV_XDICT_CAP asks
+int64_t xdict_cap_entries(int dtype, const Tuning &t) {
+  const int64_t cap_bytes = t.x_dict_cap > 0 ? t.x_dict_cap : kXdCapBytes;
+  // <= 64 KiB of LDS (and 16-bit positions) whatever x_dict_cap asks
   return std::min<int64_t>(std::min<int64_t>(cap_bytes, 64 * 1024) / (int64_t)dtype_size(dtype),
                            65536);
 }
@@ -702,8 +758,7 @@ int64_t xdict_cap_entries(int dtype) {
 int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int64_t n, int dtype,
                 unsigned flags, bool have_xwin) {
   s.xd_shape = 0;
-  const char *env = getenv("HSPMV_XDICT");
-  const int mode = env ? atoi(env) : -1;  // -1 auto, 0 off, 1 on when it fits
+  const int mode = s.tune.x_dict > 0 ? 1 : (s.tune.x_dict < 0 ? 0 : -1);  // -1 auto, 0 off, 1 on when it fits
   if (mode == 0 || (flags & HSPMV_FLAG_NO_COL16) || m == 0) return HSPMV_OK;
   if (mode < 0 && have_xwin) return HSPMV_OK;
   const int kern = kernel_for_tables(s.A.n_ssr, !s.h_tasks.empty(), flags);
@@ -715,7 +770,8 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
   if (mode < 0 && footprint <= kMallResident) return HSPMV_OK;
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
   XdPlan P;
-  if (!plan_xdict(rp, col, xdict_blocks(kern, m, s.h_tasks), long_t, xdict_cap_entries(dtype), true, P))
+  if (!plan_xdict(rp, col, xdict_blocks(kern, m, s.h_tasks, s.tune), long_t,
+                  xdict_cap_entries(dtype, s.tune), true, P))
     return HSPMV_OK;
   if (mode < 0 && 2 * P.entries > P.in_kernel_nnz) return HSPMV_OK;  // too little reuse to pay
   int rc;
@@ -730,7 +786,7 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
   s.A.cplanes = nullptr;
   s.A.n_cplanes = 0;
   s.xd_shape = kern;
-  if (kern == kCsr3) s.A.task_waves = xd_task_waves();
+  if (kern == kCsr3) s.A.task_waves = xd_task_waves(s.tune);
   s.xd_lds_bytes = (int32_t)((int64_t)P.tmax * (int64_t)sv);
   s.xd_entries = P.entries;
   s.xd_runs_n = (int64_t)P.rec.size() / 2;
@@ -749,8 +805,8 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
 // products are still added left to right from 0 (bit-identical to
 // omp_spmv for rows of <= kSerialMax (40) nonzeros per slab segment) -- which needs the
 // row's columns to be non-decreasing slab by slab (sorted rows; checked).
-// HSPMV_XSLABS=0 disables, =B forces B slabs; HSPMV_XSLAB_BYTES moves the
-// slab size.
+// Tuning.x_slabs = -1 disables, B > 0 forces B slabs; Tuning.xslab_bytes
+// (A/B) moves the slab size.
 // Irregular gathers: one gather instruction of the row kernels covers 64
 // consecutive nonzeros; when those fall on mostly distinct x cache lines
 // (random / power-law / wide-band columns) every lane is its own L2 request
@@ -786,13 +842,11 @@ constexpr int kMaxSlabs = 32;
 int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
                  int64_t n, int dtype, unsigned flags) {
   s.n_slabs = 0;
-  const char *env = getenv("HSPMV_XSLABS");
-  const int forced = env ? atoi(env) : -1;  // -1 auto, 0 off, B slabs
+  const int forced = s.tune.x_slabs < 0 ? 0 : (s.tune.x_slabs > 0 ? s.tune.x_slabs : -1);  // -1 auto, 0 off, B slabs
   if (forced == 0 || !val || m == 0 || n == 0 || (flags & 0xFu) == kVector) return HSPMV_OK;
   const int64_t nnz = rp[m];
   const double sv = (double)dtype_size(dtype);
-  double slab_bytes = kSlabBytes;
-  if (const char *e = getenv("HSPMV_XSLAB_BYTES")) slab_bytes = std::max(4096.0, atof(e));
+  const double slab_bytes = s.tune.xslab_bytes > 0 ? std::max(4096.0, s.tune.xslab_bytes) : kSlabBytes;
   int B = forced > 0 ? forced : (int)std::ceil((double)n * sv / slab_bytes);
   B = (int)std::min<int64_t>(std::min(B, kMaxSlabs), n);
   if (B < 2) return HSPMV_OK;
@@ -879,12 +933,12 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
 // columns would span more than 65535 (16-bit offsets from the chunk base).
 // Padding entries add 0 * x[base] to a dummy slot that is never read.
 // Auto: HBM-resident matrices with irregular gathers and x beyond an XCD's
-// L2 (the x-slab rule, which it replaces: C5 264 -> ~110 us);
-// HSPMV_KERNEL_CSORT forces it, HSPMV_CSORT=0 turns auto off,
-// HSPMV_CSORT_H = 1/2/4 sets the column parts, HSPMV_CSORT_U = 4/8/16 the
-// chunk.
+// L2 (the x-slab rule, which it replaces: C5 264 -> ~110 us), unless the
+// handle asks for deterministic sums (the slots add in atomic order);
+// HSPMV_KERNEL_CSORT forces it, Tuning.csort = -1 turns auto off,
+// Tuning.csort_parts = 1/2/4 sets the column parts, csort_u = 4/8/16 the
+// chunk.  The row blocks are capped by the device's LDS per workgroup.
 constexpr int32_t kCsortSlice = 2048;
-constexpr int32_t kCsortMaxSlots = kCsortMaxLds / 8 - 1;
 
 struct CsEnt {
   uint32_t col, slot, k;
@@ -901,16 +955,23 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device) != hipSuccess ||
       cus <= 0)
     cus = 256;
+  int lds_max = 0;  // the row slots must fit one workgroup's LDS on THIS device
+  if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, s.device) != hipSuccess ||
+      lds_max <= 0)
+    return HSPMV_OK;
+  lds_max = std::min(lds_max, kCsortMaxLds);
+  const Tuning &tn = s.tune;
+  const bool slot32 = dtype == HSPMV_F32 && tn.csort_slot32 == 1;
+  const int64_t slot_bytes = slot32 ? 4 : 8;
+  const int32_t max_slots = (int32_t)(lds_max / slot_bytes) - 1;
   int H = n >= 2 ? 2 : 1;
-  if (const char *e = getenv("HSPMV_CSORT_H")) {
-    const int v = atoi(e);
-    if (v == 1 || v == 2 || v == 4) H = (int)std::min<int64_t>(v, n);
-  }
+  if (tn.csort_parts == 1 || tn.csort_parts == 2 || tn.csort_parts == 4)
+    H = (int)std::min<int64_t>(tn.csort_parts, n);
   int U = dtype == HSPMV_F32 ? 16 : 8;
-  if (const char *e = getenv("HSPMV_CSORT_U")) {
-    const int v = atoi(e);
-    if (v == 4 || v == 8 || v == 16) U = v;
-  }
+  if (tn.csort_u == 4 || tn.csort_u == 8 || tn.csort_u == 16) U = tn.csort_u;
+  const int bpc = tn.csort_blocks_per_cu > 0 ? std::min(tn.csort_blocks_per_cu, 8) : 1;
+  // 16-byte entry loads: needs U a multiple of 2 (fp32 records) / 4 (fp64 indices)
+  const bool wide = tn.csort_wide == 1 && (dtype == HSPMV_F32 ? U % 2 == 0 : U % 4 == 0);
   const int64_t C = 64 * U;
   const size_t sv = dtype_size(dtype);
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
@@ -937,25 +998,41 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   }
   const int64_t n_slices = (int64_t)slice_k.size();
   // row blocks, nnz-balanced over the regular rows, capped in rows
-  const int64_t nb0 = std::max<int64_t>(1, cus / H);
+  const int64_t nb0 = std::max<int64_t>(1, (int64_t)cus * bpc / H);
   const int64_t reserve = n_slices / nb0 + 2;
-  const int64_t row_cap = kCsortMaxSlots - 1 - reserve;
+  const int64_t row_cap = max_slots - 1 - reserve;
   if (row_cap < 64) return HSPMV_OK;  // too many slices for the LDS: not this path
-  const int64_t target = std::max<int64_t>(1, (nnz - long_nnz + nb0 - 1) / nb0);
-  std::vector<int32_t> br(1, 0);
-  {
-    int64_t start = 0, acc = 0;
+  // Greedy cuts at `target` nonzeros or row_cap rows.  The target is the
+  // smallest that yields at most nb0 blocks: one more block than CUs per part
+  // would run a second round of workgroups on two CUs and double the launch
+  // (an RCM-ordered power-law matrix, whose sparse ends hit the row cap, got
+  // 129 blocks at the mean target: 291 vs 108 us).
+  auto cut = [&](int64_t target, std::vector<int32_t> *out) -> int64_t {
+    int64_t start = 0, acc = 0, nblk = 1;
+    if (out) out->assign(1, 0);
     for (int64_t r = 0; r < m; ++r) {
       if (r > start && (r - start >= row_cap || acc >= target)) {
-        br.push_back((int32_t)r);
+        if (out) out->push_back((int32_t)r);
+        ++nblk;
         start = r;
         acc = 0;
       }
       const int64_t d = rp[r + 1] - rp[r];
       acc += d > long_t ? 0 : d;
     }
-    br.push_back((int32_t)m);
+    if (out) out->push_back((int32_t)m);
+    return nblk;
+  };
+  int64_t lo = std::max<int64_t>(1, (nnz - long_nnz + nb0 - 1) / nb0), hi = std::max<int64_t>(lo, nnz + 1);
+  if (cut(lo, nullptr) > nb0) {
+    if (cut(hi, nullptr) > nb0) lo = hi;  // the row cap alone needs more blocks
+    while (lo < hi) {
+      const int64_t mid = lo + (hi - lo) / 2;
+      if (cut(mid, nullptr) <= nb0) hi = mid; else lo = mid + 1;
+    }
   }
+  std::vector<int32_t> br;
+  cut(lo, &br);
   const int64_t NB = (int64_t)br.size() - 1;
   const int64_t G = NB * H;
   if (G >= INT32_MAX) return HSPMV_OK;
@@ -1010,7 +1087,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
               E.push_back({(uint32_t)col[k], (uint32_t)(nr + (int32_t)v), k});
           std::sort(E.begin(), E.end());
           nslots[(size_t)b] = nr + (int32_t)sl.size() + 1;  // + the dummy slot
-          if (nslots[(size_t)b] > 65536 || ((int64_t)nslots[(size_t)b] + 1) * 8 > kCsortMaxLds) too_big = true;
+          if (nslots[(size_t)b] > 65536 || ((int64_t)nslots[(size_t)b] + 1) * slot_bytes > lds_max) too_big = true;
           nchunks[(size_t)b] = chunk_walk(E, [](int64_t, uint32_t, int64_t, int64_t) {});
         }
       });
@@ -1019,13 +1096,13 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   if (too_big) return HSPMV_OK;
   std::vector<int32_t> blk_c((size_t)G + 1, 0), blk_v((size_t)G + 1, 0), vslice;
   int64_t tot_chunks = 0;
-  int32_t max_slots = 1;
+  int32_t max_slots_used = 1;
   for (int64_t b = 0; b < G; ++b) {
     blk_c[(size_t)b] = (int32_t)tot_chunks;
     tot_chunks += nchunks[(size_t)b];
     blk_v[(size_t)b] = (int32_t)vslice.size();
     for (int32_t sl : wg_sl[(size_t)b]) vslice.push_back(sl);
-    max_slots = std::max(max_slots, nslots[(size_t)b]);
+    max_slots_used = std::max(max_slots_used, nslots[(size_t)b]);
   }
   blk_c[(size_t)G] = (int32_t)tot_chunks;
   blk_v[(size_t)G] = (int32_t)vslice.size();
@@ -1050,11 +1127,20 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
           auto &E = ents[(size_t)b];
           const uint32_t dummy = (uint32_t)(nslots[(size_t)b] - 1);
           const int64_t cfirst = blk_c[(size_t)b];
+          // entry q of a chunk (lane q % 64, u = q / 64) is stored at q, or,
+          // for 16-byte loads, interleaved so that one load brings the lane
+          // entries u, u+1 (fp32 records, fp64 values) or u..u+3 (fp64 indices)
+          auto at = [&](int64_t q, int per) -> int64_t {
+            if (!wide) return q;
+            const int64_t u = q / 64, lane = q % 64;
+            return (u / per) * (64 * per) + lane * per + (u % per);
+          };
           chunk_walk(E, [&](int64_t ci, uint32_t c0, int64_t i, int64_t j) {
             const int64_t ch = cfirst + ci;
             cbase[(size_t)ch] = (int32_t)c0;
             for (int64_t q = 0; q < C; ++q) {
-              const int64_t o = ch * C + q;
+              const int64_t o = ch * C + at(q, dtype == HSPMV_F32 ? 2 : 4);
+              const int64_t ov = ch * C + at(q, 2);
               uint32_t ix = dummy << 16;  // padding: 0 * x[base] into the dummy slot
               const void *vp = nullptr;
               if (i + q < j) {
@@ -1068,7 +1154,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
                 rec[(size_t)o] = ((uint64_t)vb << 32) | ix;
               } else {
                 idx[(size_t)o] = ix;
-                if (vp) memcpy(&val64[(size_t)o], vp, 8);
+                if (vp) memcpy(&val64[(size_t)ov], vp, 8);
               }
             }
           });
@@ -1107,9 +1193,10 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     s.d_cs_val = dv;
   }
   const bool direct = H == 1 && lrow.empty();
-  if (!direct) {
-    if ((rc = dev_alloc(&s.d_cs_part, 8 * (size_t)H * (size_t)m, &s.bytes))) return rc;
-    if ((rc = dev_alloc(&s.d_cs_spart, 8 * (size_t)std::max<int64_t>(n_slices, 1), &s.bytes))) return rc;
+  if (!direct) {  // partial sums in the slot type
+    if ((rc = dev_alloc(&s.d_cs_part, slot_bytes * (size_t)H * (size_t)m, &s.bytes))) return rc;
+    if ((rc = dev_alloc(&s.d_cs_spart, slot_bytes * (size_t)std::max<int64_t>(n_slices, 1), &s.bytes)))
+      return rc;
   }
   if (!lrow.empty()) {
     if ((rc = up(&s.d_cs_mask, mask)) || (rc = up(&s.d_cs_long_row, lrow)) || (rc = up(&s.d_cs_long_cs, lcs)))
@@ -1126,10 +1213,12 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.direct = direct ? 1 : 0;
   c.n_long = (int32_t)lrow.size();
   c.nontemporal = true;  // the entry stream is read once; keep x in the caches
-  if (const char *e = getenv("HSPMV_CSORT_NT")) c.nontemporal = atoi(e) != 0;
-  if (const char *e = getenv("HSPMV_CSORT_PF")) c.prefetch = atoi(e) != 0;
+  if (tn.csort_nt >= 0) c.nontemporal = tn.csort_nt != 0;  // A/B knobs
+  if (tn.csort_pf >= 0) c.prefetch = tn.csort_pf != 0;
+  c.slot32 = slot32;
+  c.wide = wide;
   c.m = m;
-  c.lds_bytes = 8 * max_slots;
+  c.lds_bytes = (int32_t)(slot_bytes * max_slots_used);
   c.blk_c = s.d_cs_blk_c;
   c.blk_r = s.d_cs_blk_r;
   c.blk_v = s.d_cs_blk_v;
@@ -1146,16 +1235,12 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   // partial sums written and read back + y
   const double xb = (double)s.x_entries * (double)sv;
   s.csort_format_bytes = (double)tot * (double)(4 + sv) + 4.0 * (double)tot_chunks + xb +
-                         (direct ? 0.0 : 16.0 * (double)H * (double)m + 16.0 * (double)n_slices) +
+                         (direct ? 0.0 : 2.0 * (double)slot_bytes * ((double)H * (double)m + (double)n_slices)) +
                          (double)sv * (double)m;
   s.A.has_csort = true;
   return HSPMV_OK;
 }
 
-int csort_mode() {
-  const char *e = getenv("HSPMV_CSORT");
-  return e ? atoi(e) : -1;  // -1 auto, 0 off, 1 whenever it can be built
-}
 
 // Host-side tables that need the columns (built at upload, while they are
 // at hand): the CSR-3 packed tasks, the block x dictionaries, and (without
@@ -1163,18 +1248,18 @@ int csort_mode() {
 // kernels.
 int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
                      int64_t n, int dtype, unsigned flags) {
-  build_tasks(rp, m, s.A.n_ssr > 0 ? &s.h_inner : nullptr, flags, s.h_tasks);
+  build_tasks(rp, m, s.A.n_ssr > 0 ? &s.h_inner : nullptr, flags, s.tune, s.h_tasks);
   s.h_xwin.clear();
   s.h_xwin_t.clear();
   int rc;
   {
     const unsigned kf = flags & 0xFu;
-    const int cm = csort_mode();
+    const int cm = s.tune.csort;  // -1 off, 0 auto, 1 whenever it can be built
     const double sv = (double)dtype_size(dtype);
     const double footprint = (double)rp[m] * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv;
     bool want = kf == kCsort || cm == 1;
-    if (!want && kf == kAuto && cm != 0 && !getenv("HSPMV_XSLABS") && footprint > kMallResident &&
-        (double)n * sv > 4.0 * 1024 * 1024)
+    if (!want && kf == kAuto && cm == 0 && !s.tune.deterministic && s.tune.x_slabs == 0 &&
+        footprint > kMallResident && (double)n * sv > 4.0 * 1024 * 1024)
       want = irregular_gathers(rp, col, m, sv);
     if (want) {
       if ((rc = build_csort(s, rp, col, val, m, n, dtype, flags))) return rc;
@@ -1190,9 +1275,9 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
     s.A.n_slabs = s.n_slabs;
     return HSPMV_OK;
   }
-  s.h_xwin = xwin_table(rp, col, m, nullptr);
+  s.h_xwin = xwin_table(rp, col, m, nullptr, s.tune);
   s.h_xwin_t.clear();
-  if (!s.h_tasks.empty()) s.h_xwin_t = xwin_table(rp, col, m, &s.h_tasks);
+  if (!s.h_tasks.empty()) s.h_xwin_t = xwin_table(rp, col, m, &s.h_tasks, s.tune);
   const int kern = kernel_for_tables(s.A.n_ssr, !s.h_tasks.empty(), flags);
   const bool have_xwin = kern == kCsr3 ? !s.h_xwin_t.empty() : !s.h_xwin.empty();
   if ((rc = build_xdict(s, rp, col, m, n, dtype, flags, have_xwin))) return rc;
@@ -1432,7 +1517,7 @@ int finish_shard(Shard &s, int dtype, unsigned flags, void *stream) {
   // 90th percentile doubled C3's waves for a 7-12 % loss, r01_ab_csr3_tasks)
   const double ssr_rows = s.mean_rows_per_ssr;
   s.plan = plan_launch(s.A, dtype, flags, ssr_rows,
-                       s.h_tasks.empty() ? 0 : (int64_t)s.h_tasks.size() - 1);
+                       s.h_tasks.empty() ? 0 : (int64_t)s.h_tasks.size() - 1, s.tune);
   int rc = build_plan_tables(s, dtype, flags);
   if (rc) return rc;
   s.x = s.d_x;
@@ -1477,7 +1562,7 @@ double time_shard(Shard &s, int dtype) {
 // elsewhere), every set is timed over a few SpMVs, and the fastest is kept;
 // the others are freed.  The kernel, its tables and every bit of y are the
 // same for all sets.  Single-GPU handles with owned arrays whose row kernel
-// (STREAM / CSR3) streams from HBM; HSPMV_PLACEMENT=K sets the number of sets
+// (STREAM / CSR3) streams from HBM; Tuning.placement_trials = K sets the number of sets
 // (0 or 1 = off); memory for the extra sets must be free, else fewer are
 // tried.  Off by default: with 4 sets per handle no faster placement turned
 // up on C3 (the first set won 8 of 8 handles; the trial sets ran 111-117 us
@@ -1488,8 +1573,7 @@ double time_shard(Shard &s, int dtype) {
 constexpr int kPlacementTrials = 0;
 
 int place_shard(Shard &s, int64_t n, int dtype) {
-  int trials = kPlacementTrials;
-  if (const char *e = getenv("HSPMV_PLACEMENT")) trials = std::max(0, std::min(8, atoi(e)));
+  int trials = s.tune.placement_trials > 0 ? std::min(8, s.tune.placement_trials) : kPlacementTrials;
   if (trials <= 1 || (s.plan.kernel != kStream && s.plan.kernel != kCsr3) || s.A.m == 0) return HSPMV_OK;
   const size_t sv = dtype_size(dtype);
   const int64_t m = s.A.m, nnz = s.A.nnz;
@@ -1581,11 +1665,20 @@ int hspmv_device_count(int *count) {
   return HSPMV_OK;
 }
 
-int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps,
-                           int device, void *stream, unsigned flags) {
-  clear_error();
-  if (!hp) return set_error(HSPMV_E_INVALID, "NULL handle pointer");
-  *hp = nullptr;
+}  // extern "C"
+
+namespace {
+
+// Sets the allocation mode of one handle creation (Tuning.contig) and
+// restores it on every return path.
+struct ContigScope {
+  explicit ContigScope(const Tuning &t) { t_contig = t.contig == 1; }
+  ~ContigScope() { t_contig = false; }
+};
+
+int create_single(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps, int device,
+                  void *stream, unsigned flags, const Tuning &tune) {
+  ContigScope contig(tune);
   const bool devptrs = (flags & HSPMV_FLAG_DEVICE_PTRS) != 0;
   if (!A) return set_error(HSPMV_E_INVALID, "matrix is NULL");
   int ndev = 0;
@@ -1598,6 +1691,7 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
   h->shards.resize(1);
   Shard &s = h->shards[0];
   s.device = device;
+  s.tune = tune;
   int rc;
   if (!devptrs) {
     if ((rc = validate_host_csr(A, true))) return rc;
@@ -1673,10 +1767,6 @@ int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_cs
   return HSPMV_OK;
 }
 
-}  // extern "C"
-
-namespace {
-
 // The row-range partition over the devices devs[0..P) (one shard each; a
 // device may appear more than once).  Distinct devices exchange x and y with
 // RCCL (one communicator per shard, ncclCommInitAll); a list that repeats a
@@ -1684,7 +1774,8 @@ namespace {
 // per device), which is how the partition, the padded y all-gather and the
 // unpadding are exercised on a one-GPU box.
 int create_sharded(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps,
-                   const std::vector<int> &devs, unsigned flags) {
+                   const std::vector<int> &devs, unsigned flags, const Tuning &tune) {
+  ContigScope contig(tune);
   const int num_gpus = (int)devs.size();
   int rc;
   if ((rc = validate_host_csr(A, true))) return rc;
@@ -1717,6 +1808,7 @@ int create_sharded(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps 
   for (int p = 0; p < num_gpus; ++p) {
     Shard &s = h->shards[p];
     s.device = devs[(size_t)p];
+    s.tune = tune;
     if ((rc = upload_shard(s, A, maps, splits[p], splits[p + 1], ssr_split[p], ssr_split[p + 1], 0,
                            flags))) {
       cleanup();
@@ -1762,9 +1854,45 @@ int check_devices(const int *devices, int n, int *ndev_out) {
   return HSPMV_OK;
 }
 
+Tuning default_tuning() {
+  Tuning t;
+  tuning_from_env(&t);  // no-op outside diagnostic builds
+  return t;
+}
+
 }  // namespace
 
 extern "C" {
+
+int hspmv_create_on_device(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps,
+                           int device, void *stream, unsigned flags) {
+  clear_error();
+  if (!hp) return set_error(HSPMV_E_INVALID, "NULL handle pointer");
+  *hp = nullptr;
+  return create_single(hp, A, maps, device, stream, flags, default_tuning());
+}
+
+int hspmv_create_ex(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps,
+                    const hspmv_options *opt) {
+  clear_error();
+  if (!hp) return set_error(HSPMV_E_INVALID, "NULL handle pointer");
+  *hp = nullptr;
+  Tuning t;
+  int rc;
+  if ((rc = tuning_from_options(opt, &t))) return rc;
+  tuning_from_env(&t);  // diagnostic builds only
+  const unsigned flags = opt ? opt->flags : 0u;
+  if (opt && opt->devices) {
+    if (flags & HSPMV_FLAG_DEVICE_PTRS)
+      return set_error(HSPMV_E_INVALID, "device pointers need a single-device handle");
+    if (opt->n_devices < 1) return set_error(HSPMV_E_INVALID, "need n_devices >= 1");
+    int ndev = 0;
+    if ((rc = check_devices(opt->devices, opt->n_devices, &ndev))) return rc;
+    return create_sharded(hp, A, maps, std::vector<int>(opt->devices, opt->devices + opt->n_devices),
+                          flags, t);
+  }
+  return create_single(hp, A, maps, opt ? opt->device : 0, opt ? opt->stream : nullptr, flags, t);
+}
 
 int hspmv_create(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps, int num_gpus,
                  unsigned flags) {
@@ -1778,10 +1906,10 @@ int hspmv_create(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *m
   if (num_gpus <= 0) num_gpus = ndev;
   if (num_gpus > ndev)
     return set_error(HSPMV_E_NODEV, "%d GPUs requested, %d visible", num_gpus, ndev);
-  if (num_gpus == 1) return hspmv_create_on_device(hp, A, maps, 0, nullptr, flags);
+  if (num_gpus == 1) return create_single(hp, A, maps, 0, nullptr, flags, default_tuning());
   std::vector<int> devs((size_t)num_gpus);
   for (int p = 0; p < num_gpus; ++p) devs[(size_t)p] = p;
-  return create_sharded(hp, A, maps, devs, flags);
+  return create_sharded(hp, A, maps, devs, flags, default_tuning());
 }
 
 int hspmv_create_sharded(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps,
@@ -1794,7 +1922,8 @@ int hspmv_create_sharded(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3
   if (!devices || n_shards < 1) return set_error(HSPMV_E_INVALID, "need n_shards >= 1 devices");
   int ndev = 0, rc;
   if ((rc = check_devices(devices, n_shards, &ndev))) return rc;
-  return create_sharded(hp, A, maps, std::vector<int>(devices, devices + n_shards), flags);
+  return create_sharded(hp, A, maps, std::vector<int>(devices, devices + n_shards), flags,
+                        default_tuning());
 }
 
 // Shards that share a device (no communicators): the same exchanges as
@@ -1843,30 +1972,44 @@ static int copy_exchange(hspmv_handle *h, bool x_bcast) {
   return rc;
 }
 
+}  // extern "C"
+
+// One RCCL group over every shard's communicator: op(p) enqueues shard p's
+// part.  The group is always closed (ncclGroupEnd) before returning, also
+// when an enqueue fails -- an open group would swallow the calling thread's
+// next RCCL calls.
+template <typename Op>
+static int rccl_group(hspmv_handle *h, const char *what, Op op) {
+  ncclResult_t r = ncclGroupStart();
+  if (r != ncclSuccess) return set_error(HSPMV_E_RCCL, "ncclGroupStart: %s", ncclGetErrorString(r));
+  ncclResult_t first = ncclSuccess;
+  for (size_t p = 0; p < h->shards.size() && first == ncclSuccess; ++p) first = op(p);
+  r = ncclGroupEnd();
+  if (first != ncclSuccess) return set_error(HSPMV_E_RCCL, "%s: %s", what, ncclGetErrorString(first));
+  if (r != ncclSuccess) return set_error(HSPMV_E_RCCL, "%s (ncclGroupEnd): %s", what, ncclGetErrorString(r));
+  return HSPMV_OK;
+}
+
+extern "C" {
+
 static int bcast_x(hspmv_handle *h) {
   if (!h->sharded) return HSPMV_OK;
   if (h->comms.empty()) return copy_exchange(h, true);
   const ncclDataType_t dt = h->dtype == HSPMV_F64 ? ncclFloat64 : ncclFloat32;
-  RCCL_TRY(ncclGroupStart());
-  for (size_t p = 0; p < h->shards.size(); ++p) {
+  return rccl_group(h, "ncclBroadcast(x)", [&](size_t p) {
     Shard &s = h->shards[p];
-    RCCL_TRY(ncclBroadcast(h->shards[0].d_x, s.d_x, (size_t)h->n, dt, 0, h->comms[p], s.stream));
-  }
-  RCCL_TRY(ncclGroupEnd());
-  return HSPMV_OK;
+    return ncclBroadcast(h->shards[0].d_x, s.d_x, (size_t)h->n, dt, 0, h->comms[p], s.stream);
+  });
 }
 
 static int gather_y(hspmv_handle *h) {
   if (!h->sharded) return HSPMV_OK;
   if (h->comms.empty()) return copy_exchange(h, false);
   const ncclDataType_t dt = h->dtype == HSPMV_F64 ? ncclFloat64 : ncclFloat32;
-  RCCL_TRY(ncclGroupStart());
-  for (size_t p = 0; p < h->shards.size(); ++p) {
+  return rccl_group(h, "ncclAllGather(y)", [&](size_t p) {
     Shard &s = h->shards[p];
-    RCCL_TRY(ncclAllGather(s.d_y, s.d_yfull, (size_t)h->max_rows, dt, h->comms[p], s.stream));
-  }
-  RCCL_TRY(ncclGroupEnd());
-  return HSPMV_OK;
+    return ncclAllGather(s.d_y, s.d_yfull, (size_t)h->max_rows, dt, h->comms[p], s.stream);
+  });
 }
 
 int hspmv_set_x(hspmv_handle *h, const void *x_host) {
@@ -2069,10 +2212,26 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->placement_trials = (int32_t)s.place_us.size();
   out->placement_pick = s.place_pick;
   for (size_t k = 0; k < s.place_us.size() && k < 8; ++k) out->placement_us[k] = s.place_us[k];
+  out->deterministic = 1;
+  for (auto &sh : h->shards) out->deterministic &= sh.plan.kernel == kCsort ? 0 : 1;
+  out->csr3_plan = s.plan.kernel != kCsr3 ? 0
+                   : s.h_tasks.empty() ? HSPMV_CSR3_PLAN_SSR
+                   : csr3_fill(s.tune) ? HSPMV_CSR3_PLAN_ALIGNED : HSPMV_CSR3_PLAN_PACKED;
+  out->csort_slot_bytes = s.plan.kernel == kCsort ? (s.dp.cs.slot32 ? 4 : 8) : 0;
   return HSPMV_OK;
 }
 
-int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, unsigned flags,
+int hspmv_get_info_sized(hspmv_handle *h, hspmv_info *out, uint32_t out_size) {
+  clear_error();
+  if (!out) return set_error(HSPMV_E_INVALID, "NULL output");
+  hspmv_info full;
+  int rc = hspmv_get_info(h, &full);
+  if (rc) return rc;
+  memcpy(out, &full, std::min<size_t>(out_size, sizeof(full)));
+  return HSPMV_OK;
+}
+
+int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, const hspmv_options *opt,
                      int64_t cap_entries, int64_t *n_blocks, int64_t *n_records, int32_t *blk,
                      int32_t *runs, uint16_t *pos) {
   clear_error();
@@ -2080,23 +2239,26 @@ int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, unsigned f
   *n_blocks = 0;
   *n_records = 0;
   int rc;
+  Tuning tune;
+  if ((rc = tuning_from_options(opt, &tune))) return rc;
+  const unsigned flags = opt ? opt->flags : 0u;
   if ((rc = validate_host_csr(A, true))) return rc;
   if ((rc = validate_host_maps(maps, A->m))) return rc;
   std::vector<int32_t> tasks;
   const bool csr3 = maps && maps->n_ssr > 0;
   if (csr3) {
     const std::vector<int32_t> inner(maps->inner, maps->inner + maps->n_sr + 1);
-    build_tasks(A->row_ptr, A->m, &inner, flags, tasks);
+    build_tasks(A->row_ptr, A->m, &inner, flags, tune, tasks);
   } else {
-    build_tasks(A->row_ptr, A->m, nullptr, flags, tasks);
+    build_tasks(A->row_ptr, A->m, nullptr, flags, tune, tasks);
   }
   const int kern = kernel_for_tables(csr3 ? maps->n_ssr : 0, !tasks.empty(), flags);
   if ((kern != kStream && kern != kCsr3) || A->m == 0) return HSPMV_OK;
-  if (cap_entries <= 0) cap_entries = xdict_cap_entries(A->dtype);
+  if (cap_entries <= 0) cap_entries = xdict_cap_entries(A->dtype, tune);
   XdPlan P;
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
   const bool fill = blk || runs || pos;
-  if (!plan_xdict(A->row_ptr, A->col_idx, xdict_blocks(kern, A->m, tasks), long_t,
+  if (!plan_xdict(A->row_ptr, A->col_idx, xdict_blocks(kern, A->m, tasks, tune), long_t,
                   std::min<int64_t>(cap_entries, 65536), fill, P))
     return HSPMV_OK;  // some block exceeds the cap: no dictionary (n_blocks = 0)
   *n_blocks = (int64_t)P.blk.size() - 1;

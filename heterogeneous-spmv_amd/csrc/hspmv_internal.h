@@ -36,6 +36,38 @@ struct DevCSR {
   bool has_csort = false;     // column-sorted row blocks were built (irregular gathers)
 };
 
+// Planner choices of one handle.  The first block mirrors hspmv_options
+// (include/hspmv.h; 0 = the library's choice); the second holds A/B-only
+// knobs that product builds never change: only a diagnostic build
+// (make diag-env: -DHSPMV_ENV_KNOBS) reads them, and the public fields, from
+// HSPMV_* environment variables (tuning_from_env, hspmv_api.cpp), so a
+// production handle's kernel choice cannot move with the environment.
+struct Tuning {
+  int csr3_plan = 0;        // 0/1 aligned 64-row tasks, 2 packed super-rows, 3 workgroup per SSR
+  int task_nnz = 0;         // wave-task nonzero budget (0: 2048)
+  int x_windows = 0;        // -1 off, 0 auto
+  int x_dict = 0;           // -1 off, 0 auto, 1 whenever it fits
+  int x_dict_cap = 0;       // LDS bytes per dictionary block (0: 20 KiB; <= 64 KiB)
+  int x_slabs = 0;          // -1 off, 0 auto, B > 0 forced
+  int col16_group = 0;      // -1 off, 0 auto, 1 whenever it fits
+  int csort = 0;            // -1 off, 0 auto, 1 whenever it can be built
+  int csort_parts = 0;      // 0 auto, 1/2/4
+  int csort_u = 0;          // 0 auto, 4/8/16
+  int stream_waves = 0;     // 0 auto, 1/2/4
+  int deterministic = 0;    // 1: only kernels whose y bits never depend on scheduling
+  int placement_trials = 0; // 0/1 off, K <= 8 array sets
+  // A/B only (diagnostic builds)
+  int contig = 0;           // hipDeviceMallocContiguous allocations
+  int xd_waves = 0;         // packed CSR3 tasks per dictionary block (0: 4; 8)
+  double xslab_bytes = 0;   // x bytes per slab (0: 2 MiB)
+  int csort_nt = -1, csort_pf = -1;      // -1: the library's choice
+  int csort_blocks_per_cu = 0;           // row blocks per CU and part (0: 1)
+  int csort_slot32 = -1;                 // fp32 LDS row slots (fp32 data)
+  int csort_wide = -1;                   // 16-byte entry loads (interleaved layout)
+  int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
+  int dyn_lds = 0;
+};
+
 constexpr int kC16Shift = 8;  // 256 nonzeros per column-base block
 constexpr int kXWin = 256;    // largest LDS-staged x window of a row group (entries)
 
@@ -58,13 +90,15 @@ struct DevCsort {
   int32_t n_wg = 0, H = 1, u = 16, direct = 0, n_long = 0;
   bool nontemporal = true;
   bool prefetch = false;  // next chunk's entries loaded during this chunk's gathers
+  bool slot32 = false;    // fp32 LDS row slots and partials (fp32 data; A/B)
+  bool wide = false;      // 16-byte entry loads (host-interleaved layout)
   int64_t m = 0;
   int32_t lds_bytes = 0;
   const int32_t *blk_c = nullptr, *blk_r = nullptr, *blk_v = nullptr, *vslice = nullptr;
   const int32_t *cbase = nullptr;
   const void *ent = nullptr;  // fp32: {idx, val} records; fp64: idx
   const void *val = nullptr;  // fp64 values (nullptr for fp32)
-  double *part = nullptr, *spart = nullptr;
+  void *part = nullptr, *spart = nullptr;  // partial sums in the slot type
   const uint32_t *long_mask = nullptr;
   const int32_t *long_row = nullptr, *long_cs = nullptr;
 };
@@ -128,7 +162,7 @@ struct LaunchPlan {
 // rows_per_ssr: mean rows per super-super-row (CSR-3 workgroup-per-SSR plan);
 // packed_tasks > 0: CSR-3 tasks packed from super-rows (4 per workgroup).
 LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_per_ssr,
-                       int64_t packed_tasks);
+                       int64_t packed_tasks, const Tuning &t);
 
 // STREAM / CSR3 row kernels (stream_f32.hip / stream_f64.hip).
 hipError_t launch_rows_f32(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p,

@@ -232,7 +232,7 @@ int pick_u(double nnz_per_pass, int dtype, bool slabs) {
 }  // namespace
 
 LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_per_ssr,
-                       int64_t packed_tasks) {
+                       int64_t packed_tasks, const Tuning &t) {
   LaunchPlan p;
   const unsigned k = flags & 0xFu;
   p.nontemporal = (flags & (1u << 12)) != 0;  // HSPMV_FLAG_NONTEMPORAL
@@ -310,10 +310,8 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
       // 211.2 -> 207.5).  Four (the dictionaries' 256-row blocks) with x
       // dictionaries; profiles/r01_ab_stream_w.jsonl.
       p.waves_per_block = A.has_xdict ? 4 : ((footprint <= 192.0 * 1024 * 1024 || A.has_xwin) ? 1 : 2);
-      if (const char *e = getenv("HSPMV_STREAM_W")) {
-        const int w = atoi(e);
-        if ((w == 1 || w == 2 || w == 4) && !A.has_xdict) p.waves_per_block = w;
-      }
+      if ((t.stream_waves == 1 || t.stream_waves == 2 || t.stream_waves == 4) && !A.has_xdict)
+        p.waves_per_block = t.stream_waves;
       p.blocks = (waves + p.waves_per_block - 1) / p.waves_per_block;
       break;
     }
@@ -382,10 +380,10 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   // r02r_ab_pf.jsonl)
   if (!p.prefetch && dtype == 1 && p.kernel == kCsr3 && A.has_xdict_tasks && !forced_u)
     p.prefetch = true;
-  if (const char *e = getenv("HSPMV_PF")) p.prefetch = atoi(e) != 0;
-  if (const char *e = getenv("HSPMV_YNT")) p.y_nt = atoi(e) != 0;
-  if (const char *e = getenv("HSPMV_NT")) p.nontemporal = atoi(e) != 0;
-  if (const char *e = getenv("HSPMV_DYNLDS")) p.dyn_lds = atoi(e);
+  if (t.pf >= 0) p.prefetch = t.pf != 0;  // A/B knobs (diagnostic builds only)
+  if (t.y_nt >= 0) p.y_nt = t.y_nt != 0;
+  if (t.nt >= 0) p.nontemporal = t.nt != 0;
+  p.dyn_lds = t.dyn_lds;
   return p;
 }
 

@@ -114,7 +114,51 @@ class Info(C.Structure):
                 ("x_dict_entries", C.c_int64), ("x_slabs", C.c_int32),
                 ("col16_group", C.c_int32), ("csort_parts", C.c_int32),
                 ("placement_trials", C.c_int32), ("placement_pick", C.c_int32),
-                ("placement_us", C.c_double * 8)]
+                ("placement_us", C.c_double * 8),
+                ("deterministic", C.c_int32), ("csr3_plan", C.c_int32),
+                ("csort_slot_bytes", C.c_int32), ("reserved", C.c_int32)]
+
+
+CSR3_PLANS = {"auto": 0, "aligned": 1, "packed": 2, "ssr": 3}
+
+
+class Options(C.Structure):
+    """hspmv_options (include/hspmv.h): explicit planner choices for
+    hspmv_create_ex; 0 everywhere = the library's choice."""
+    _fields_ = [("struct_size", C.c_uint32), ("flags", C.c_uint32),
+                ("devices", C.POINTER(C.c_int)), ("n_devices", C.c_int32),
+                ("device", C.c_int32), ("stream", C.c_void_p),
+                ("csr3_plan", C.c_int32), ("task_nnz", C.c_int32), ("x_windows", C.c_int32),
+                ("x_dict", C.c_int32), ("x_dict_cap", C.c_int32), ("x_slabs", C.c_int32),
+                ("col16_group", C.c_int32), ("csort", C.c_int32), ("csort_parts", C.c_int32),
+                ("csort_chunk_u", C.c_int32), ("stream_waves", C.c_int32),
+                ("deterministic", C.c_int32), ("placement_trials", C.c_int32)]
+
+    # planner fields a caller may set by name (SpMV(..., options={...}))
+    TUNABLE = ("csr3_plan", "task_nnz", "x_windows", "x_dict", "x_dict_cap", "x_slabs",
+               "col16_group", "csort", "csort_parts", "csort_chunk_u", "stream_waves",
+               "deterministic", "placement_trials")
+
+
+def make_options(flags: int, tuning: dict | None, *, device: int = 0, stream=None,
+                 devices=None) -> Options:
+    o = Options()
+    o.struct_size = C.sizeof(Options)
+    o.flags = flags
+    o.device = int(device)
+    o.stream = stream
+    if devices is not None:
+        arr = (C.c_int * len(devices))(*[int(d) for d in devices])
+        o._devices_keepalive = arr
+        o.devices = C.cast(arr, C.POINTER(C.c_int))
+        o.n_devices = len(devices)
+    for k, v in (tuning or {}).items():
+        if k not in Options.TUNABLE:
+            raise ValueError(f"unknown hspmv option {k!r} (one of {', '.join(Options.TUNABLE)})")
+        if k == "csr3_plan" and isinstance(v, str):
+            v = CSR3_PLANS[v]
+        setattr(o, k, int(v))
+    return o
 
 
 _P = C.c_void_p
@@ -126,6 +170,8 @@ SIGNATURES = {
                                          C.c_int, _P, C.c_uint]),
     "hspmv_create_sharded": (C.c_int, [C.POINTER(_H), C.POINTER(Csr), C.POINTER(Csr3Maps),
                                        C.POINTER(C.c_int), C.c_int, C.c_uint]),
+    "hspmv_create_ex": (C.c_int, [C.POINTER(_H), C.POINTER(Csr), C.POINTER(Csr3Maps),
+                                  C.POINTER(Options)]),
     "hspmv_set_x": (C.c_int, [_H, _P]),
     "hspmv_bind_x_device": (C.c_int, [_H, _P]),
     "hspmv_bind_y_device": (C.c_int, [_H, _P]),
@@ -137,6 +183,7 @@ SIGNATURES = {
     "hspmv_get_y": (C.c_int, [_H, _P]),
     "hspmv_exchange": (C.c_int, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "hspmv_get_info": (C.c_int, [_H, C.POINTER(Info)]),
+    "hspmv_get_info_sized": (C.c_int, [_H, C.POINTER(Info), C.c_uint32]),
     "hspmv_destroy": (None, [_H]),
     "hspmv_read_csr": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(CsrBuf)]),
     "hspmv_read_csr3": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(CsrBuf), C.POINTER(Csr3Buf)]),
@@ -154,7 +201,7 @@ SIGNATURES = {
                                          C.POINTER(Csr3Buf), _P]),
     "hspmv_csr3_params": (C.c_int, [C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hspmv_partition_rows": (C.c_int, [C.c_int64, _P, C.POINTER(Csr3Maps), C.c_int, _P]),
-    "hspmv_xdict_plan": (C.c_int, [C.POINTER(Csr), C.POINTER(Csr3Maps), C.c_uint, C.c_int64,
+    "hspmv_xdict_plan": (C.c_int, [C.POINTER(Csr), C.POINTER(Csr3Maps), C.POINTER(Options), C.c_int64,
                                    C.POINTER(C.c_int64), C.POINTER(C.c_int64), _P, _P, _P]),
     "hspmv_alg_bytes": (C.c_double, [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int64]),
     "hspmv_device_count": (C.c_int, [C.POINTER(C.c_int)]),

@@ -255,7 +255,7 @@ def partition_rows(row_ptr: np.ndarray, parts: int, maps: Optional[Csr3Maps] = N
 
 
 def xdict_plan(A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, kernel: str = "auto",
-               cap_entries: int = 0, split: bool = True):
+               cap_entries: int = 0, split: bool = True, options: Optional[dict] = None):
     """Block x dictionaries the library would build for A (hspmv_xdict_plan):
     (blk, runs, pos) with runs as an (n_records, 2) array of {x_start,
     lds_off}, or None when some workgroup exceeds cap_entries (0 = the
@@ -263,9 +263,10 @@ def xdict_plan(A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, kernel: str = "
     cs = A.c_struct()
     ms = maps.c_struct() if maps is not None else None
     flags = _KERNELS[kernel] | (0 if split else _lib.FLAG_NO_SPLIT)
+    opt = _lib.make_options(flags, options)
     nb, nr = C.c_int64(), C.c_int64()
     L = lib()
-    args = (C.byref(cs), C.byref(ms) if ms is not None else None, flags, int(cap_entries))
+    args = (C.byref(cs), C.byref(ms) if ms is not None else None, C.byref(opt), int(cap_entries))
     check(L.hspmv_xdict_plan(*args, C.byref(nb), C.byref(nr), None, None, None), "xdict_plan")
     if nb.value == 0:
         return None
@@ -300,7 +301,9 @@ class SpMV:
     for "vector" (0 = auto).  ``device``/``stream``: single-device handle on that
     HIP device / hipStream_t (as an int); ``devices``: row-range shards on that
     device list (hspmv_create_sharded; devices may repeat); otherwise
-    ``num_gpus`` GPUs with the row-range partition.
+    ``num_gpus`` GPUs with the row-range partition.  ``options``: explicit
+    planner choices (hspmv_options fields by name, e.g. ``{"csr3_plan": "ssr",
+    "deterministic": 1}``; handle created with hspmv_create_ex).
     """
 
     def __init__(self, A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, num_gpus: int = 1,
@@ -308,7 +311,8 @@ class SpMV:
                  device: Optional[int] = None, stream: Optional[int] = None,
                  xcd_remap: Optional[bool] = None, split_rows: bool = True, chunk_u: int = 0,
                  prefetch: Optional[bool] = None, xcd_chunk: int = 0, groups_per_wave: int = 0,
-                 col16: Optional[bool] = None, devices: Optional[list] = None):
+                 col16: Optional[bool] = None, devices: Optional[list] = None,
+                 options: Optional[dict] = None):
         self.A = A
         self.maps = maps
         self.dtype = A.val.dtype
@@ -325,7 +329,14 @@ class SpMV:
         cs = A.c_struct()
         ms = maps.c_struct() if maps is not None else None
         h = C.c_void_p()
-        if devices is not None:  # row-range shards on an explicit device list
+        if options:  # explicit planner choices: hspmv_create_ex
+            if num_gpus != 1 and devices is None:
+                devices = list(range(num_gpus))
+            opt = _lib.make_options(flags, options, device=0 if device is None else device,
+                                    stream=stream, devices=devices)
+            rc = lib().hspmv_create_ex(C.byref(h), C.byref(cs),
+                                       C.byref(ms) if ms is not None else None, C.byref(opt))
+        elif devices is not None:  # row-range shards on an explicit device list
             dl = (C.c_int * len(devices))(*[int(d) for d in devices])
             rc = lib().hspmv_create_sharded(C.byref(h), C.byref(cs),
                                             C.byref(ms) if ms is not None else None, dl,
@@ -346,7 +357,8 @@ class SpMV:
                     lanes: int = 0, nontemporal: bool = False, xcd_remap: Optional[bool] = None,
                     split_rows: bool = True, chunk_u: int = 0,
                     prefetch: Optional[bool] = None, xcd_chunk: int = 0,
-                    groups_per_wave: int = 0, col16: Optional[bool] = None) -> "SpMV":
+                    groups_per_wave: int = 0, col16: Optional[bool] = None,
+                    options: Optional[dict] = None) -> "SpMV":
         """Handle over caller-owned DEVICE arrays (HSPMV_FLAG_DEVICE_PTRS):
         csr_dev/maps_dev hold device pointers; A_meta supplies m, n, dtype."""
         self = cls.__new__(cls)
@@ -359,9 +371,10 @@ class SpMV:
                  | (0 if split_rows else _lib.FLAG_NO_SPLIT) | (chunk_u << _lib.U_SHIFT)
                  | (_lib.FLAG_PREFETCH if prefetch else 0))
         h = C.c_void_p()
-        check(lib().hspmv_create_on_device(C.byref(h), C.byref(csr_dev),
-                                           C.byref(maps_dev) if maps_dev is not None else None,
-                                           int(device), stream, flags), "hspmv_create_on_device")
+        opt = _lib.make_options(flags, options, device=device, stream=stream)
+        check(lib().hspmv_create_ex(C.byref(h), C.byref(csr_dev),
+                                    C.byref(maps_dev) if maps_dev is not None else None,
+                                    C.byref(opt)), "hspmv_create_ex")
         self._h = h
         return self
 

@@ -58,7 +58,9 @@ class Shard:
 #   c3h configs[2]  alt: hugebubbles-00000 stand-in, CSR fp64
 #   c4  configs[3]  CSR fp64, banded m = 2e7 split over the ranks (strong)
 #   c5  configs[4]  CSR-3 fp32, power-law m = 2e6 (MI355X grouping)
-CONFIGS = ("c2", "c3", "c3h", "c4", "c5")
+#   c5r configs[4]  the same matrix RCM-permuted (the reference's .rcm.csr
+#                   input ordering, helpers/converter.m:8,14)
+CONFIGS = ("c2", "c3", "c3h", "c4", "c5", "c5r")
 
 
 def default_config(world: int) -> str:
@@ -90,15 +92,17 @@ def _whole_matrix(config: str, dtype):
     if config == "c3h":
         A = gen.honeycomb(4280, 4280, dtype=dtype)
         return A, None, "hugebubbles-00000 stand-in: honeycomb 4280^2 RCM (fp64 CSR)"
-    if config == "c5":
-        A = gen.powerlaw(2_000_000, seed=1234, dtype=dtype)
+    if config in ("c5", "c5r"):
+        rcm = config == "c5r"
+        A = gen.powerlaw(2_000_000, seed=1234, dtype=dtype, rcm=rcm)
         return A, build_csr3_maps(A, *csr3_params(A.nnz / A.m, "mi355x")), \
-            "power-law m=2e6, Pareto alpha=1.5, seed 1234 (fp32 CSR-3)"
+            ("power-law m=2e6, Pareto alpha=1.5, seed 1234" + (", RCM-permuted" if rcm else "")
+             + " (fp32 CSR-3)")
     raise ValueError(config)
 
 
 def config_dtype(config: str):
-    return np.float32 if config == "c5" else np.float64
+    return np.float32 if config in ("c5", "c5r") else np.float64
 
 
 def laplace2d_row_nnz(nx: int, ny: int) -> np.ndarray:
@@ -163,7 +167,7 @@ def build_shard(config: str, rank: int, world: int, dtype=None) -> Shard:
        c4: banded m = 2e7 (BASELINE configs[3]) split over the ranks (strong).
        small: 5-pt Laplacian 64 x 64 per rank (tests)."""
     dtype = config_dtype(config) if dtype is None else dtype
-    if config in ("c3", "c3h", "c5"):
+    if config in ("c3", "c3h", "c5", "c5r"):
         A, maps, name = _whole_matrix(config, dtype)
         splits = partition_rows(A.row_ptr, world, maps)
         if maps is not None:
@@ -222,7 +226,7 @@ def gather_y(y_local, splits: np.ndarray):
     out = torch.empty(pad * world, dtype=y_local.dtype, device=buf.device)
     dist.all_gather_into_tensor(out, buf)
     parts = [out[r * pad: r * pad + int(rows[r])] for r in range(world)]
-    return torch.cat(parts)
+    return torch.cat(parts).to(y_local.device)  # on the caller's device whatever the backend
 
 
 def checksum_ok(A: CsrMatrix, x: np.ndarray, y: np.ndarray, seed: int = 99) -> tuple[bool, float]:

@@ -10,7 +10,9 @@ stand-in with the shape the reference benchmarks:
 * C4     banded: m = 20,000,000, 10 nonzeros per row at r+o, o drawn without
          replacement from [-32, 32], seed 11, values U(-1,1).
 * C5     power-law: row degree min(4*(Pareto(1.5)+1), m/10), random columns,
-         symmetrised + diagonal, seed 1234.
+         symmetrised + diagonal, seed 1234; c5r = the same matrix
+         RCM-permuted, the ordering the reference benchmarks its inputs in
+         (helpers/converter.m:8,14: symrcm -> .mtx.rcm.csr).
 
 Generators that may be sharded take a row range [r0, r1) so that each rank of
 a row-range partition builds only its own rows (global columns).
@@ -151,9 +153,13 @@ def banded(m: int, per_row: int = 10, half: int = 32, seed: int = 11, r0: int = 
                      np.concatenate(vas).astype(dtype))
 
 
-def powerlaw(m: int, alpha: float = 1.5, seed: int = 1234, dtype=np.float32) -> CsrMatrix:
+def powerlaw(m: int, alpha: float = 1.5, seed: int = 1234, dtype=np.float32,
+             rcm: bool = False) -> CsrMatrix:
     """Scale-free rows: degree min(4*(Pareto(alpha)+1), m/10), random columns,
-    symmetrised (A + A^T pattern) plus the diagonal, values U(-1,1)."""
+    symmetrised (A + A^T pattern) plus the diagonal, values U(-1,1).  rcm:
+    the same matrix (same values) symmetrically permuted by reverse
+    Cuthill-McKee, as the reference's converter orders its inputs
+    (helpers/converter.m:8,14)."""
     import scipy.sparse as sp
     rng = np.random.default_rng(seed)
     deg = np.minimum((4 * (rng.pareto(alpha, m) + 1)).astype(np.int64), max(m // 10, 1))
@@ -166,6 +172,11 @@ def powerlaw(m: int, alpha: float = 1.5, seed: int = 1234, dtype=np.float32) -> 
     S.sum_duplicates()
     S.sort_indices()
     S.data = rng.uniform(-1.0, 1.0, S.nnz).astype(np.float64)
+    if rcm:
+        from scipy.sparse.csgraph import reverse_cuthill_mckee
+        perm = reverse_cuthill_mckee(S, symmetric_mode=True)
+        S = S[perm][:, perm].tocsr()
+        S.sort_indices()
     return CsrMatrix.from_scipy(S, dtype)
 
 

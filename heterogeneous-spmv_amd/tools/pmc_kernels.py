@@ -13,7 +13,7 @@ import sys
 vals = {}
 for f in glob.glob(sys.argv[1] + "/p*/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        k = re.sub(r"\(.*", "", r["Kernel_Name"])
+        k = re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))
         m = re.search(r"seg_read<(\d+), (\w+)>", r["Kernel_Name"])
         if m:
             k = f"seg_read<{m.group(1)},{m.group(2)}>"

@@ -106,10 +106,10 @@ def build(cfg):
         A = hspmv.CsrMatrix.from_scipy(S, np.float64)
         return A, None, (f"mixed rows: {m} rows, Pareto lengths 8..4000 (mean {A.nnz / m:.0f}), "
                          "band +-4000, CSR fp64")
-    if cfg == "c5":
-        A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32)
+    if cfg in ("c5", "c5r"):  # c5r: the same matrix RCM-permuted (helpers/converter.m:8,14)
+        A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32, rcm=cfg == "c5r")
         maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
-        return A, maps, "C5 power-law 2e6 rows CSR-3 fp32"
+        return A, maps, "C5 power-law 2e6 rows CSR-3 fp32" + (" RCM-permuted" if cfg == "c5r" else "")
     raise ValueError(cfg)
 
 

@@ -35,7 +35,7 @@ extern "C" {
 #endif
 
 #define HSPMV_VERSION_MAJOR 0
-#define HSPMV_VERSION_MINOR 1
+#define HSPMV_VERSION_MINOR 2  /* 0.2: hspmv_options, info.deterministic */
 
 /* ---------------------------------------------------------------- status */
 #define HSPMV_OK 0
@@ -146,9 +146,19 @@ typedef struct {
   int32_t csort_parts; /* CSORT: column parts H of the row blocks (0 = the
                           handle does not use the column-sorted kernel)     */
   int32_t placement_trials; /* array sets timed at creation (0 = none: see
-                               HSPMV_PLACEMENT in hspmv_create_on_device)  */
+                               hspmv_options.placement_trials)             */
   int32_t placement_pick;   /* the set kept (0 = the first allocation)      */
   double placement_us[8];   /* each set's mean SpMV time at creation, us    */
+  /* since 0.2 */
+  int32_t deterministic;    /* 1: y is bit-identical run to run (every kernel
+                               but CSORT, whose LDS row sums add in atomic
+                               order: fp32 y may differ in the last bit where
+                               an fp64 sum sits at an fp32 rounding tie, fp64
+                               y in the last bits of rows it sums)          */
+  int32_t csr3_plan;        /* CSR3 kernel: the HSPMV_CSR3_PLAN_* it runs;
+                               0 for the other kernels                      */
+  int32_t csort_slot_bytes; /* CSORT: LDS row-slot width (8 = fp64 sums)    */
+  int32_t reserved;
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
@@ -158,17 +168,21 @@ typedef struct hspmv_handle hspmv_handle;
 #define HSPMV_KERNEL_VECTOR 1u /* L lanes (sub-wave) per row, shuffle sum  */
 #define HSPMV_KERNEL_STREAM 2u /* wave per 64-row group, LDS-staged,
                                   ordered per-row sums (bit-exact vs CPU)  */
-#define HSPMV_KERNEL_CSR3 3u   /* 64-row aligned wave tasks, 4 per
-                                  workgroup (HSPMV_TASK_FILL=0: super-rows
-                                  packed into <= 64-row tasks; or one
-                                  workgroup per super-super-row:
-                                  HSPMV_CSR3_PLAN=ssr)                    */
+#define HSPMV_KERNEL_CSR3 3u   /* wave tasks planned from the CSR-3 maps,
+                                  4 per workgroup (hspmv_options.csr3_plan:
+                                  64-row aligned tasks, super-rows packed
+                                  into <= 64-row tasks, or one workgroup
+                                  per super-super-row)                     */
 #define HSPMV_KERNEL_CSORT 4u  /* column-sorted row blocks: each workgroup
                                   walks its rows' nonzeros in column order,
-                                  fp64 LDS row sums (irregular gathers; not
-                                  bitwise vs omp_spmv: see csort.hip). AUTO
-                                  picks it for HBM-resident matrices whose
-                                  gathers are irregular                      */
+                                  fp64 LDS row sums (irregular gathers).
+                                  NOT bitwise vs omp_spmv and NOT bit-
+                                  identical run to run: the sums add in
+                                  LDS-atomic order (csort.hip,
+                                  hspmv_info.deterministic).  AUTO picks it
+                                  for HBM-resident matrices whose gathers
+                                  are irregular, unless
+                                  hspmv_options.deterministic = 1          */
 #define HSPMV_KERNEL_MASK 0xFu
 /* lanes per row for VECTOR: HSPMV_LANES(L), L in {1,2,4,8,16,32,64}; 0=auto */
 #define HSPMV_LANES_SHIFT 4
@@ -217,7 +231,58 @@ typedef struct hspmv_handle hspmv_handle;
  * unchanged, so y is bit-identical.  HSPMV_FLAG_NO_COL16 turns it off;
  * hspmv_info.col16 / format_bytes report what a handle uses. */
 
+/* ---------------------------------------------------------------- options */
+/* Explicit planner choices for hspmv_create_ex.  Zero-initialise, set
+ * struct_size = sizeof(hspmv_options) (a caller built against an older,
+ * shorter struct passes its own size; the fields it lacks read as 0), then
+ * set what you need: every 0 means "the library's choice", which is what
+ * hspmv_create / _on_device / _sharded use.  These replace the HSPMV_*
+ * environment variables of earlier versions: a production handle's kernel
+ * and tables depend only on the matrix, the flags and these options (only a
+ * diagnostic build, `make diag-env`, reads the environment). */
+#define HSPMV_CSR3_PLAN_AUTO 0    /* = ALIGNED                                */
+#define HSPMV_CSR3_PLAN_ALIGNED 1 /* 64-row aligned wave tasks, 4 per
+                                     workgroup (the maps bound the shards)   */
+#define HSPMV_CSR3_PLAN_PACKED 2  /* whole super-rows (inner map) packed into
+                                     <= 64-row wave tasks                    */
+#define HSPMV_CSR3_PLAN_SSR 3     /* one workgroup per super-super-row (outer
+                                     map), its super-rows split over W waves
+                                     by nonzeros: the reference's cuSpMV_3
+                                     mapping (csrk.cu:245-319)               */
+typedef struct {
+  uint32_t struct_size;   /* sizeof(hspmv_options) of the caller            */
+  uint32_t flags;         /* HSPMV_KERNEL_* | HSPMV_FLAG_* (hspmv_create)    */
+  const int *devices;     /* row-range shard p on devices[p] (may repeat), as
+                             hspmv_create_sharded; NULL: one shard on device */
+  int32_t n_devices;
+  int32_t device;         /* single-shard handle: the HIP device ...         */
+  void *stream;           /* ... and its hipStream_t (NULL: library-owned)  */
+  int32_t csr3_plan;      /* HSPMV_CSR3_PLAN_*                              */
+  int32_t task_nnz;       /* CSR3 wave-task nonzero budget (0: 2048)        */
+  int32_t x_windows;      /* -1: no LDS x windows; 0 auto                   */
+  int32_t x_dict;         /* -1 off, 0 auto, 1 whenever it fits the cap     */
+  int32_t x_dict_cap;     /* LDS bytes per dictionary block (0: 20 KiB)     */
+  int32_t x_slabs;        /* -1 off, 0 auto, B > 0: B column slabs          */
+  int32_t col16_group;    /* -1 off, 0 auto, 1 whenever every group fits    */
+  int32_t csort;          /* -1 off, 0 auto, 1 whenever it can be built     */
+  int32_t csort_parts;    /* column parts of the csort row blocks: 0 auto,
+                             1, 2, 4                                        */
+  int32_t csort_chunk_u;  /* csort entries per lane per chunk: 0, 4, 8, 16  */
+  int32_t stream_waves;   /* STREAM waves per workgroup: 0 auto, 1, 2, 4    */
+  int32_t deterministic;  /* 1: never pick a kernel whose y bits depend on
+                             the hardware's scheduling (HSPMV_KERNEL_CSORT
+                             adds its row sums in LDS-atomic order); every
+                             other kernel gives the same bits on every run */
+  int32_t placement_trials; /* array placements timed at creation (0/1
+                               off, K <= 8; see hspmv_create_on_device)    */
+} hspmv_options;
+
 /* ---------------------------------------------------------------- handle */
+/* hspmv_create_on_device / hspmv_create_sharded with explicit options
+ * (opt == NULL: all defaults on device 0). */
+int hspmv_create_ex(hspmv_handle **h, const hspmv_csr *A, const hspmv_csr3_maps *maps,
+                    const hspmv_options *opt);
+
 /* Upload A (and optional CSR-3 maps) to num_gpus devices (0 = all visible).
  * With num_gpus > 1 the rows are partitioned into nnz-balanced contiguous
  * ranges (on super-super-row boundaries when maps are given), x is
@@ -243,8 +308,8 @@ int hspmv_create_sharded(hspmv_handle **h, const hspmv_csr *A,
  * the row pointers, column stream, values, x and y are copied into up to
  * three further allocations, each copy is timed over a few SpMVs and the
  * fastest placement is kept (the others are freed; y bits do not depend on
- * it).  Opt-in: environment HSPMV_PLACEMENT=K (K <= 8 sets; default off --
- * measured no gain); hspmv_info reports the times.  With trials
+ * it).  Opt-in: hspmv_options.placement_trials = K (K <= 8 sets; default
+ * off -- measured no gain); hspmv_info reports the times.  With trials
  * on, creation launches the kernel. */
 int hspmv_create_on_device(hspmv_handle **h, const hspmv_csr *A,
                            const hspmv_csr3_maps *maps, int device,
@@ -278,6 +343,9 @@ int hspmv_get_y(hspmv_handle *h, void *y_host);
 int hspmv_exchange(hspmv_handle *h, double *bcast_x_s, double *gather_y_s);
 
 int hspmv_get_info(hspmv_handle *h, hspmv_info *out);
+/* The same for a caller whose hspmv_info may be older (shorter) than this
+ * library's: fills min(out_size, sizeof(hspmv_info)) bytes. */
+int hspmv_get_info_sized(hspmv_handle *h, hspmv_info *out, uint32_t out_size);
 void hspmv_destroy(hspmv_handle *h);
 
 /* ---------------------------------------------------------------- formats */
@@ -357,8 +425,9 @@ int hspmv_partition_rows(int64_t m, const int32_t *row_ptr,
  * staged_b[pos[k]] with staged_b[lds_off + i] = x[x_start + i].  Call with
  * NULL buffers for the sizes.  *n_blocks = 0: some block needs more than
  * cap_entries (<= 0: the library's LDS cap for A's dtype), so no dictionary.
+ * opt (NULL = defaults) supplies the kernel flags and the CSR-3 plan.
  * Not a reference interface: the test and diagnostic view of the format. */
-int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, unsigned flags,
+int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, const hspmv_options *opt,
                      int64_t cap_entries, int64_t *n_blocks, int64_t *n_records,
                      int32_t *blk, int32_t *runs, uint16_t *pos);
 double hspmv_alg_bytes(int64_t m, int64_t n, int64_t nnz, int dtype,

@@ -69,7 +69,7 @@ def test_struct_layouts_match_the_header(tmp_path):
     offsets: a mismatch makes hspmv_get_info / hspmv_run write past the
     caller's struct (a C program built against an older header crashes the
     same way -- rebuild the tools after a header change)."""
-    structs = {"hspmv_info": _lib.Info, "hspmv_timing": _lib.Timing}
+    structs = {"hspmv_info": _lib.Info, "hspmv_timing": _lib.Timing, "hspmv_options": _lib.Options}
     lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "hspmv.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')

@@ -10,7 +10,11 @@ sum bit for bit.  What is checked instead, on the same seeded inputs:
 * fp32 data: y is the fp32 rounding of the fp64 sum of the exact products, so
   within half an fp32 ulp (+ the fp64 summation error) of the exact sum, and
   within omp_spmv's own fp32 summation error of the reference's y;
-* repeatability, long rows cut into slices (first/last/adjacent rows, and with
+* run-to-run behaviour: fp32 y equal except at fp32 rounding ties, fp64 y
+  within the fp64 rounding of the sum (the atomic order varies), reported as
+  hspmv_info.deterministic = 0; hspmv_options.deterministic keeps AUTO off
+  csort and refuses an explicit csort;
+* long rows cut into slices (first/last/adjacent rows, and with
   HSPMV_FLAG_NO_SPLIT kept whole), empty rows and blocks, 1/2/4 column parts,
   chunk sizes, an Inf in x (padding must not spread it), and the planner's
   auto choice (irregular gathers only).
@@ -79,28 +83,25 @@ def _matrices():
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("parts", ["1", "2", "4"])
-def test_csort_matches_oracle(dtype, parts, monkeypatch):
-    monkeypatch.setenv("HSPMV_CSORT_H", parts)
+def test_csort_matches_oracle(dtype, parts):
     for name, A in _matrices():
         A = A.astype(dtype)
         x = gen.rand_x(A.n, 17).astype(dtype)
-        y, info = run(A, x, kernel="csort")
+        y, info = run(A, x, kernel="csort", options={"csort_parts": int(parts)})
         assert info["kernel_name"] == "csort", name
         assert info["csort_parts"] == min(int(parts), A.n), name
         assert info["n_split_rows"] == int((np.diff(A.row_ptr) > 4096).sum()), name
         check(A, x, y)
 
 
-@pytest.mark.parametrize("u", ["4", "8", "16"])
-def test_csort_chunk_sizes_and_nontemporal(u, monkeypatch):
-    monkeypatch.setenv("HSPMV_CSORT_U", u)
-    A = gen.powerlaw(50_000, seed=9, dtype=np.float32)
-    x = gen.rand_x(A.n, 3).astype(np.float32)
-    for nt in ("0", "1"):
-        monkeypatch.setenv("HSPMV_CSORT_NT", nt)
-        y, info = run(A, x, kernel="csort")
-        assert info["chunk_u"] == int(u)
-        check(A, x, y)
+@pytest.mark.parametrize("u", [4, 8, 16])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_csort_chunk_sizes(u, dtype):
+    A = gen.powerlaw(50_000, seed=9, dtype=dtype)
+    x = gen.rand_x(A.n, 3).astype(dtype)
+    y, info = run(A, x, kernel="csort", options={"csort_chunk_u": u})
+    assert info["chunk_u"] == u
+    check(A, x, y)
 
 
 def test_csort_long_rows_whole_and_sliced():
@@ -125,6 +126,38 @@ def test_csort_repeatable_fp32():
     for y in ys[1:]:
         assert np.mean(ys[0] == y) > 0.9999
     check(A, x, ys[0])
+
+
+def test_csort_run_to_run_fp64_and_deterministic_option():
+    """fp64: every run is within the fp64 rounding of the sum of the same
+    products (only the atomic order of the additions varies), so two runs
+    differ by at most a few fp64 ulps of sum|a x| per row -- and the handle
+    says so (info.deterministic = 0).  deterministic=1 keeps AUTO on a row
+    kernel (bit-identical run to run and to omp_spmv on short rows) and
+    refuses an explicit csort."""
+    A = gen.powerlaw(2_000_000, seed=12, dtype=np.float64)
+    x = gen.rand_x(A.n, 8)
+    lens = np.diff(A.row_ptr)
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    with hspmv.SpMV(A) as op:
+        info = op.info
+        ys = [op(x) for _ in range(3)]
+    assert info["kernel_name"] == "csort" and info["deterministic"] == 0
+    for y in ys[1:]:
+        d = np.abs(y - ys[0])
+        assert np.all(d <= 2.0 * (lens + 1) * 2.0 ** -53 * absrow)
+    check(A, x, ys[0])
+    with hspmv.SpMV(A, options={"deterministic": 1}) as op:
+        info = op.info
+        yd = [op(x) for _ in range(2)]
+    assert info["kernel_name"] != "csort" and info["deterministic"] == 1
+    assert np.array_equal(yd[0], yd[1])
+    y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    short = lens <= 40
+    assert np.array_equal(yd[0][short], y64[short])
+    assert fp64_tol_ok(yd[0], y64, absrow)
+    with pytest.raises(hspmv.HspmvError):
+        hspmv.SpMV(A, kernel="csort", options={"deterministic": 1})
 
 
 def test_csort_padding_does_not_spread_inf():

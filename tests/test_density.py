@@ -88,13 +88,12 @@ def test_density_band_matches_oracle(d, dtype):
     check(A, x, ys)
 
 
-def test_task_budget_env(monkeypatch):
+def test_task_budget_option():
     A = banded(300, nnz=600_000)
     x = gen.rand_x(A.n, 3)
     tasks = {}
     for budget in ("300", "2048", "1000000"):
-        monkeypatch.setenv("HSPMV_TASK_NNZ", budget)
-        y, info = run(A, x)
+        y, info = run(A, x, options={"task_nnz": int(budget)})
         check(A, x, y)
         tasks[budget] = info["wave_tasks"] if info["kernel_name"] == "csr3" else 0
     # ~one row per task at 300 (the clipped edge rows pair up), ~6 rows at

@@ -100,24 +100,21 @@ def test_golden_csr3_fixtures(manifest):
 
 @pytest.mark.parametrize("plan", ["aligned", "packed", "ssr"])
 @pytest.mark.parametrize("waves_case", [(7, 8), (20, 10), (64, 4), (1, 1), (400, 2), (2, 100)])
-def test_csr3_map_sizes(waves_case, plan, monkeypatch):
+def test_csr3_map_sizes(waves_case, plan):
     """Any map granularity (tiny super-rows, one-row super-rows, huge SSRs
     that need several waves and several 64-row groups, super-rows of more
     than 64 rows) gives the same y, under the three CSR-3 task plans
     (64-row aligned tasks, super-rows packed into tasks, a workgroup per
     super-super-row)."""
-    if plan == "ssr":
-        monkeypatch.setenv("HSPMV_CSR3_PLAN", "ssr")
-    if plan == "packed":
-        monkeypatch.setenv("HSPMV_TASK_FILL", "0")
     ssrs, srs = waves_case
     # the banded matrix's tasks take the LDS x-window path (span <= 256 columns)
     for A in (gen.laplace2d(300, 200), gen.powerlaw(30000, seed=11, dtype=np.float64),
               gen.banded(20000, per_row=10, half=32, seed=3, dtype=np.float64)):
         maps = hspmv.build_csr3_maps(A, ssrs, srs)
         x = gen.rand_x(A.n, 5)
-        y, info = gpu_spmv(A, x, maps)
+        y, info = gpu_spmv(A, x, maps, options={"csr3_plan": plan})
         assert info["kernel_name"] == "csr3"
+        assert info["csr3_plan"] == hspmv._lib.CSR3_PLANS[plan]
         if plan != "ssr":  # aligned 64-row groups, or whole super-rows per task (<= 64 rows)
             sr_rows = np.diff(maps.inner)
             lower = int(np.ceil(A.m / 64))
@@ -132,12 +129,11 @@ def test_csr3_map_sizes(waves_case, plan, monkeypatch):
 
 
 @pytest.mark.parametrize("xwin", ["0", "1"])
-def test_x_window_variants_identical(xwin, monkeypatch):
+def test_x_window_variants_identical(xwin):
     """Global gathers and LDS x windows give the same bits (the windows only
     change where x[col] is read from), for STREAM and for packed CSR-3
     tasks; groups whose columns do not fit a window mix in."""
-    if xwin == "0":
-        monkeypatch.setenv("HSPMV_XWIN", "0")
+    opts = {"x_windows": -1} if xwin == "0" else None
     rng = np.random.default_rng(4)
     A0 = gen.banded(40000, per_row=10, half=32, seed=6)
     # every 7th group gets a far column, so some groups do not fit
@@ -148,7 +144,7 @@ def test_x_window_variants_identical(xwin, monkeypatch):
     x = gen.rand_x(A.n, 12)
     maps = hspmv.build_csr3_maps(A, 7, 8)
     for mp in (None, maps):
-        y, info = gpu_spmv(A, x, mp)
+        y, info = gpu_spmv(A, x, mp, options=opts)
         assert info["x_windows"] == int(xwin)
         check_fp64(A, x, y, exact_rows=slice(None))
 
@@ -284,13 +280,33 @@ def test_config_c4_banded_shard_fp64():
     assert info["x_windows"] == 1 or info["x_dict"] == 1
 
 
-def test_config_c5_powerlaw_csr3_fp32(monkeypatch):
+def test_config_c4_full_matrix_one_gpu():
+    """BASELINE configs[3] whole: the 2e7-row, 2e8-nonzero banded matrix on
+    ONE GPU (the N = 1 point of the strong-scaling curve, bench.py
+    scaling_reference).  Every row has <= 10 nonzeros (<= 40: the ordered
+    sums), so y must equal the oracle's omp_spmv restatement bit for bit."""
+    from hspmv import dist as hdist
+    sh = hdist.build_shard("c4", 0, 1)
+    A = sh.A
+    assert A.m == 20_000_000 and 199_999_000 < A.nnz <= 200_000_000
+    assert int(np.diff(A.row_ptr).max()) <= SERIAL_MAX
+    x = gen.rand_x(A.n, 11)
+    y, info = gpu_spmv(A, x)
+    y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    assert info["kernel_name"] in ("stream", "csr3") and info["deterministic"] == 1
+    assert np.array_equal(y.view(np.uint64), y64.view(np.uint64))
+    ok, rel = hdist.checksum_ok(A, x, y)
+    assert ok, rel
+
+
+def test_config_c5_powerlaw_csr3_fp32():
     """BASELINE configs[4]: power-law fp32 with CSR-3 maps.  Its random
     columns make the gathers irregular, so AUTO runs the column-sorted row
     blocks (csort: fp64 row sums, rounded once): y is checked against the
     exact (fp64) sums to an fp32 rounding and against omp_spmv's fp32 sums
-    within their summation error.  The x-slab CSR-3 path (HSPMV_XSLABS) stays
-    available and bitwise on short rows."""
+    within their summation error.  The x-slab CSR-3 path (options x_slabs)
+    stays available and bitwise on short rows, and deterministic=1 keeps the
+    row kernels."""
     A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32)
     maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
     x = gen.rand_x(A.n, 9).astype(np.float32)
@@ -304,8 +320,7 @@ def test_config_c5_powerlaw_csr3_fp32(monkeypatch):
     y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
     err = np.abs(y.astype(np.float64) - y32.astype(np.float64))
     assert np.all(err <= (lens + 2) * 2.0 ** -23 * absrow + 1e-30)
-    monkeypatch.setenv("HSPMV_XSLABS", "4")
-    ys, info = gpu_spmv(A, x, maps)
+    ys, info = gpu_spmv(A, x, maps, options={"x_slabs": 4})
     assert info["kernel_name"] == "csr3" and info["x_slabs"] == 4
     ok = short_rows(A)
     assert np.array_equal(ys[ok].view(np.uint32), y32[ok].view(np.uint32))
@@ -373,7 +388,7 @@ def test_chunk_u_and_remap_variants():
             assert fp64_tol_ok(y, y64, absrow)
 
 
-def test_borrowed_device_arrays(monkeypatch):
+def test_borrowed_device_arrays():
     """HSPMV_FLAG_DEVICE_PTRS: the handle reads caller-owned device arrays
     (torch tensors here) and caller-bound x / y; the host tables (x slabs
     included: the values are read back for the slab-major copy) are built
@@ -396,10 +411,9 @@ def test_borrowed_device_arrays(monkeypatch):
         op.synchronize()
         check_fp64(A, x, yd.cpu().numpy(), exact_rows=short_rows(A) if kernel != "vector" else None)
         op.close()
-    monkeypatch.setenv("HSPMV_XSLABS", "3")
     for mdev, kernel in ((None, "stream"), (ms, "csr3")):
         yd.zero_()
-        op = hspmv.SpMV.from_device(cs, mdev, A, device=0, kernel=kernel)
+        op = hspmv.SpMV.from_device(cs, mdev, A, device=0, kernel=kernel, options={"x_slabs": 3})
         assert op.info["x_slabs"] == 3
         op.bind_x_device(xd.data_ptr())
         op.bind_y_device(yd.data_ptr())
@@ -407,7 +421,6 @@ def test_borrowed_device_arrays(monkeypatch):
         op.synchronize()
         check_fp64(A, x, yd.cpu().numpy(), exact_rows=short_rows(A))
         op.close()
-    monkeypatch.delenv("HSPMV_XSLABS")
     bad = hspmv._lib.Csr(A.m, A.n, A.nnz, rp.data_ptr(), 0, val.data_ptr(), 1)
     with pytest.raises(hspmv.HspmvError, match="E_INVALID"):
         hspmv.SpMV.from_device(bad, None, A, device=0)
@@ -431,13 +444,13 @@ def _band_random(m, per_row, half, seed):
                            rng.uniform(-1, 1, m * per_row))
 
 
-def test_col16_offsets_bitwise_and_fallback(monkeypatch):
+def test_col16_offsets_bitwise_and_fallback():
     """16-bit column offsets give the same y bit for bit as 32-bit columns,
     through STREAM, CSR3, prefetch and split rows, in both encodings:
     per-256-nonzero block bases + p high-bit planes (forced here with
-    HSPMV_COL16G=0, p <= 8; p grows with a block's column span and a matrix
+    options col16_group=-1, p <= 8; p grows with a block's column span and a matrix
     needing more than 8 planes keeps 32-bit columns), and one base per
-    64-row STREAM group or packed CSR3 task (HSPMV_COL16G=1) when every
+    64-row STREAM group or packed CSR3 task (col16_group=1) when every
     group spans < 65536.
     By default these small (Infinity-Cache-resident) matrices use the group
     bases where they fit and 32-bit columns otherwise."""
@@ -453,10 +466,8 @@ def test_col16_offsets_bitwise_and_fallback(monkeypatch):
         maps = hspmv.build_csr3_maps(A, 20, 10)
         for kw, mp in [(dict(kernel="stream"), None), (dict(kernel="stream", prefetch=True), None),
                        (dict(kernel="csr3"), maps), (dict(kernel="stream", chunk_u=2), None)]:
-            monkeypatch.setenv("HSPMV_COL16G", "0")
-            y16, i16 = gpu_spmv(A, x, mp, col16=True, **kw)
-            monkeypatch.setenv("HSPMV_COL16G", "1")
-            y16g, i16g = gpu_spmv(A, x, mp, col16=True, **kw)
+            y16, i16 = gpu_spmv(A, x, mp, col16=True, options={"col16_group": -1}, **kw)
+            y16g, i16g = gpu_spmv(A, x, mp, col16=True, options={"col16_group": 1}, **kw)
             y32, i32 = gpu_spmv(A, x, mp, col16=False, **kw)
             assert i32["col16"] == 0 and i32["format_bytes"] == i32["alg_bytes"]
             assert i16["col16_group"] == 0
@@ -471,7 +482,6 @@ def test_col16_offsets_bitwise_and_fallback(monkeypatch):
             assert np.array_equal(y16, y32), kw
             assert np.array_equal(y16g, y32), kw
         check_fp64(A, x, y16, exact_rows=short_rows(A))
-        monkeypatch.delenv("HSPMV_COL16G")
         _, idef = gpu_spmv(A, x)
         assert idef["col16_group"] == int(group_fits)
         assert idef["col16"] == int(group_fits)  # small: block offsets only when forced
@@ -491,14 +501,14 @@ def _few_random(m, n, per_row, seed, dtype=np.float64):
                            rng.uniform(-1, 1, m * per_row).astype(dtype))
 
 
-def test_xdict_bitwise_and_fallback(monkeypatch):
-    """Block x dictionaries (HSPMV_XDICT=1 forces them on these small
+def test_xdict_bitwise_and_fallback():
+    """Block x dictionaries (options x_dict=1 forces them on these small
     matrices): each workgroup stages the x runs its rows reference in LDS
     and gathers from there through 16-bit positions.  y is bit-identical to
     the 32-bit-column path through STREAM, CSR3 (packed tasks), prefetch,
     nontemporal loads, U = 2 and split rows, in fp64 and fp32; a matrix whose
     blocks exceed the LDS cap falls back (x_dict = 0) with the same y."""
-    big = str(64 * 1024)  # LDS bytes per block (default cap: 20 KiB)
+    big = 64 * 1024  # LDS bytes per block (default cap: 20 KiB)
     cases = [(gen.laplace2d(300, 200), True, None),
              (gen.stencil27(20), True, None),
              (gen.banded(30000, per_row=10, half=32, seed=5), True, None),
@@ -507,10 +517,6 @@ def test_xdict_bitwise_and_fallback(monkeypatch):
              (gen.powerlaw(200000, seed=3, dtype=np.float64), False, None),   # > cap: off
              (_few_random(3000, 8000, 2, 4), None, big)]                    # gap bridging
     for A, want, cap in cases:
-        if cap:
-            monkeypatch.setenv("HSPMV_XDICT_CAP", cap)
-        else:
-            monkeypatch.delenv("HSPMV_XDICT_CAP", raising=False)
         for dt in (np.float64, np.float32):
             Ad = A.astype(dt)
             x = gen.rand_x(A.n, 9).astype(dt)
@@ -519,10 +525,8 @@ def test_xdict_bitwise_and_fallback(monkeypatch):
                            (dict(kernel="csr3"), maps), (dict(kernel="stream", chunk_u=2), None),
                            (dict(kernel="csr3", nontemporal=True), maps),
                            (dict(kernel="csr3", prefetch=True), maps)]:
-                monkeypatch.setenv("HSPMV_XDICT", "1")
-                yd, idd = gpu_spmv(Ad, x, mp, **kw)
-                monkeypatch.setenv("HSPMV_XDICT", "0")
-                y0, i0 = gpu_spmv(Ad, x, mp, col16=False, **kw)
+                yd, idd = gpu_spmv(Ad, x, mp, options={"x_dict": 1, "x_dict_cap": cap or 0}, **kw)
+                y0, i0 = gpu_spmv(Ad, x, mp, col16=False, options={"x_dict": -1}, **kw)
                 assert i0["x_dict"] == 0 and i0["x_dict_entries"] == 0
                 if want is not None and not (want is False and dt == np.float32):
                     assert idd["x_dict"] == int(want), (kw, dt, idd["x_dict"])
@@ -531,7 +535,6 @@ def test_xdict_bitwise_and_fallback(monkeypatch):
                 assert np.array_equal(yd.view(np.uint8), y0.view(np.uint8)), (kw, dt)
             if dt == np.float64:
                 check_fp64(Ad, x, yd, exact_rows=short_rows(Ad))
-    monkeypatch.delenv("HSPMV_XDICT")
     # default on these small (Infinity-Cache-resident) matrices: no dictionary
     A = gen.stencil27(20)
     _, idef = gpu_spmv(A, gen.rand_x(A.n, 1))
@@ -549,8 +552,8 @@ def _slab_exact_rows(A, slabs):
     return (seg.max(axis=1, initial=0) <= SERIAL_MAX) & (lens <= 4096)
 
 
-def test_xslabs_bitwise_rows_and_fallback(monkeypatch):
-    """x slabs (HSPMV_XSLABS=B forces B column slabs): the row kernel runs
+def test_xslabs_bitwise_rows_and_fallback():
+    """x slabs (options x_slabs=B forces B column slabs): the row kernel runs
     once per slab over a slab-major copy, each pass continuing the rows
     from y.  Rows whose slab segments are all <= 32 nonzeros are
     bit-identical to the oracle (fp64 restatement, fp32 reference loop),
@@ -560,7 +563,6 @@ def test_xslabs_bitwise_rows_and_fallback(monkeypatch):
              _split_row_matrix(), gen.laplace2d(1, 1), gen.laplace2d(300, 200)]
     for A in cases:
         for slabs in (2, 5):
-            monkeypatch.setenv("HSPMV_XSLABS", str(slabs))
             exact = _slab_exact_rows(A, min(slabs, A.n))
             for dt in (np.float64, np.float32):
                 Ad = A.astype(dt)
@@ -570,7 +572,7 @@ def test_xslabs_bitwise_rows_and_fallback(monkeypatch):
                 for kw, mp in [(dict(kernel="stream"), None), (dict(kernel="csr3"), maps),
                                (dict(kernel="stream", prefetch=True), None),
                                (dict(kernel="stream", chunk_u=2, nontemporal=True), None)]:
-                    ys, info = gpu_spmv(Ad, x, mp, **kw)
+                    ys, info = gpu_spmv(Ad, x, mp, options={"x_slabs": slabs}, **kw)
                     want = min(slabs, A.n) if min(slabs, A.n) >= 2 else 0
                     assert info["x_slabs"] == want, (kw, info["x_slabs"])
                     assert np.array_equal(ys[exact].view(np.uint8), ref[exact].view(np.uint8)), kw
@@ -587,15 +589,13 @@ def test_xslabs_bitwise_rows_and_fallback(monkeypatch):
     ci = A.col_idx.copy()
     ci[A.row_ptr[10]] = 2400  # row 10: [2400, 10, 11, 60] -> slabs 2, 0, 0, 0
     Au = hspmv.CsrMatrix(A.m, A.n, A.row_ptr, ci, A.val)
-    monkeypatch.setenv("HSPMV_XSLABS", "3")
     x = gen.rand_x(A.n, 2)
-    yu, iu = gpu_spmv(Au, x)
+    yu, iu = gpu_spmv(Au, x, options={"x_slabs": 3})
     assert iu["x_slabs"] == 0
     check_fp64(Au, x, yu, exact_rows=short_rows(Au))
     # the vector kernel never uses slabs; default on small matrices: none
-    _, iv = gpu_spmv(A, x, kernel="vector")
+    _, iv = gpu_spmv(A, x, kernel="vector", options={"x_slabs": 3})
     assert iv["x_slabs"] == 0
-    monkeypatch.delenv("HSPMV_XSLABS")
     _, idef = gpu_spmv(gen.powerlaw(100000, seed=3, dtype=np.float64), gen.rand_x(100000, 1))
     assert idef["x_slabs"] == 0
 
@@ -640,8 +640,8 @@ def test_full_size_fp32_bitwise_vs_reference_omp_spmv(cfg):
     assert np.all(err <= (np.diff(A.row_ptr) + 2) * 2.0 ** -23 * absrow + 1e-30)
 
 
-def test_stream_workgroup_sizes_identical(monkeypatch):
-    """STREAM with 1, 2 and 4 waves per workgroup (HSPMV_STREAM_W; the
+def test_stream_workgroup_sizes_identical():
+    """STREAM with 1, 2 and 4 waves per workgroup (options stream_waves; the
     planner picks 1 for cache-resident / x-windowed matrices, 2 otherwise,
     4 with x dictionaries): bit-identical y, including x windows, several
     groups per wave, split rows and a row count that is not a multiple of
@@ -662,12 +662,10 @@ def test_stream_workgroup_sizes_identical(monkeypatch):
                    dict(kernel="stream", col16=True)):
             ys = []
             for w in ("1", "2", "4"):
-                monkeypatch.setenv("HSPMV_STREAM_W", w)
-                y, info = gpu_spmv(A, x, **kw)
+                y, info = gpu_spmv(A, x, options={"stream_waves": int(w)}, **kw)
                 assert info["waves_per_block"] == int(w), (kw, w, info["waves_per_block"])
                 ys.append(y)
             assert all(np.array_equal(ys[0].view(np.uint8), v.view(np.uint8)) for v in ys[1:]), kw
         check_fp64(A, x, ys[0], exact_rows=short_rows(A))
-    monkeypatch.delenv("HSPMV_STREAM_W")
     _, info = gpu_spmv(gen.laplace2d(300, 200), gen.rand_x(60000, 1))
     assert info["waves_per_block"] == 1  # cache-resident: one wave per workgroup

@@ -106,16 +106,15 @@ def check_plan(A, plan, bounds, split=True, cap=None):
 
 @pytest.mark.parametrize("fill", [True, False])
 @pytest.mark.parametrize("case", ["lap", "stencil", "banded", "random", "longrows"])
-def test_plan_addresses_every_nonzero(case, fill, monkeypatch):
-    if not fill:
-        monkeypatch.setenv("HSPMV_TASK_FILL", "0")
+def test_plan_addresses_every_nonzero(case, fill):
+    opts = None if fill else {"csr3_plan": "packed"}
     A = {"lap": lambda: gen.laplace2d(120, 90),
          "stencil": lambda: gen.stencil27(14),
          "banded": lambda: gen.banded(5000, per_row=10, half=32, seed=5),
          "random": lambda: _random_rows(1500, 6000, 3, 4),   # many short runs: gaps bridged
          "longrows": _long_rows}[case]()
     for kernel, maps in [("stream", None), ("csr3", hspmv.build_csr3_maps(A, 7, 8))]:
-        plan = hspmv.xdict_plan(A, maps, kernel=kernel, cap_entries=65536)
+        plan = hspmv.xdict_plan(A, maps, kernel=kernel, cap_entries=65536, options=opts)
         assert plan is not None
         check_plan(A, plan, block_rows(A, maps, kernel, fill))
     if case == "longrows":  # without split rows every row is in the dictionary
