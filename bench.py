@@ -28,7 +28,9 @@ Extra fields on the line:
   cold         the same SpMV with the 256 MiB Infinity Cache evicted before
                every launch (a 512 MiB read)
   comm         RCCL x broadcast / y all-gather / halo-exchange times (N > 1),
-               timed separately, and the end-to-end rates they imply
+               timed separately, and the end-to-end rates they imply; plus the
+               y all-gather OVERLAPPED with the SpMV (rows in K chunks, chunk k
+               gathered while chunks k+1.. compute; hspmv.dist.OverlappedGather)
   csr3_maps_plans  (CSR-3 workloads) the same SpMV under the two maps-driven
                CSR-3 plans, timed in the same process: "packed" (whole
                super-rows of the inner map packed into <= 64-row wave tasks)
@@ -89,6 +91,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="budget of the CPU-baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-plans", action="store_true",
+                    help="skip the csr3_maps_plans legs (maps-driven CSR-3 plans)")
     ap.add_argument("--no-scaling-ref", action="store_true",
                     help="at N = 1, skip timing the N > 1 configuration (C4) on this GPU")
     ap.add_argument("--dry-run", action="store_true",
@@ -411,6 +415,58 @@ def csr3_maps_plans(args, A, maps, x, y_ref, stream, device):
     return out
 
 
+def overlapped_gather(args, A, shard, x, y, stream, device, info, world, chunks: int = 4):
+    """One SpMV + the y all-gather, overlapped: this rank's rows in `chunks`
+    nnz-balanced handles launched back to back on the SpMV stream, each
+    chunk's rows all-gathered (async, RCCL's stream) right after its kernel,
+    so the exchange of chunk k overlaps chunks k+1..  Timed end to end
+    (launch of the first chunk to the assembled full y), max over ranks; y
+    checked against the plain gather of the headline y."""
+    import torch
+
+    import hspmv
+    from hspmv import dist as hdist
+    sub = hdist.chunk_splits(A, chunks)
+    og = hdist.OverlappedGather(np.diff(sub), device="cuda", dtype=y.dtype)
+    ops = []
+    for k in range(chunks):
+        a, b = int(sub[k]), int(sub[k + 1])
+        op = hspmv.SpMV(A.rows(a, b), device=device, stream=stream.cuda_stream)
+        op.bind_x_device(x.data_ptr())
+        op.bind_y_device(og.buffer(k).data_ptr())
+        ops.append(op)
+
+    def once():
+        for k, op in enumerate(ops):
+            op.spmv()
+            og.start(k)
+        return og.finish()
+
+    ref = hdist.gather_y(y, shard.splits)
+    for _ in range(2):
+        yfull = once()
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(5):
+        barrier(world)
+        t0 = time.perf_counter()
+        yfull = once()
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) * 1e3)
+        barrier(world)
+    ms = reduce_over_ranks(float(np.median(times)), world, "max")
+    if info["deterministic"]:
+        ok = bool(torch.equal(yfull, ref))
+    else:  # csort shards: the same y within the summation order
+        ok = bool(torch.allclose(yfull, ref, rtol=1e-5 if y.dtype == torch.float32 else 1e-12, atol=0))
+    ok = reduce_over_ranks(1.0 if ok else 0.0, world, "sum") == world
+    for op in ops:
+        op.close()
+    return ({"chunks": chunks, "ms": round(ms, 4),
+             "end_to_end_overlapped_gflops": round(2.0 * shard.nnz_global / (ms * 1e-3) * 1e-9, 3),
+             "y_equal_to_plain_gather": ok}, ok)
+
+
 # ------------------------------------------------------------------ main
 
 def main():
@@ -523,6 +579,8 @@ def main():
         halo_ok = bool(torch.equal(xw, x[halo.lo:halo.hi]))
         ok_all = ok_all and reduce_over_ranks(1.0 if halo_ok else 0.0, world, "sum") == world
         del xw
+        overlap, ov_ok = overlapped_gather(args, A, shard, x, y, stream, local, info, world)
+        ok_all = ok_all and ov_ok
 
     flops_step = 2.0 * shard.nnz_global
     alg_local = info["alg_bytes"]  # x counted as the distinct columns this shard reads
@@ -533,7 +591,7 @@ def main():
     traffic = load_traffic(workload_key) if rank == 0 else None
 
     plans = None
-    if maps is not None and info["kernel_name"] == "csr3":
+    if maps is not None and info["kernel_name"] == "csr3" and not args.no_plans:
         plans = csr3_maps_plans(args, A, maps, x, y, stream, local)
         ok_all = ok_all and reduce_over_ranks(
             1.0 if all(p["y_bitwise_equal_to_headline"] for p in plans.values()) else 0.0,
@@ -605,7 +663,8 @@ def main():
                       "gflops": round(2.0 * A.nnz / cold_s * 1e-9, 3),
                       "note": "a 512 MiB read before each launch evicts the Infinity Cache"}
                      if cold_s else None),
-            "comm": {"bcast_x_ms": round(bcast_ms, 3) if world > 1 else None,
+            "comm": {"overlap": overlap if world > 1 else None,
+                     "bcast_x_ms": round(bcast_ms, 3) if world > 1 else None,
                      "gather_y_ms": round(gather_ms, 3) if gather_ms is not None else None,
                      "halo_x_ms": round(halo_ms, 4) if halo_ms is not None else None,
                      "x_bytes": shard.n_global * x.element_size(),

@@ -122,9 +122,9 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   S *acc = reinterpret_cast<S *>(smem);
   constexpr int NW = kCsortThreads / kWave;
   const int b = blockIdx.x;
-  const int rb = b / H, h = b - rb * H;
+  const int h = b % H;  // the column part; its rows: the part's own row block
   const int32_t c0 = blk_c[b], c1 = blk_c[b + 1];
-  const int32_t r0 = blk_r[rb], r1 = blk_r[rb + 1];
+  const int32_t r0 = blk_r[2 * b], r1 = blk_r[2 * b + 1];
   const int32_t v0 = blk_v[b], v1 = blk_v[b + 1];
   const int32_t nr = r1 - r0, nv = v1 - v0;
   for (int32_t i = threadIdx.x; i <= nr + nv; i += kCsortThreads) acc[i] = S(0);  // + dummy

@@ -950,7 +950,6 @@ struct CsEnt {
 int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
                 int64_t n, int dtype, unsigned flags) {
   if (m == 0 || n == 0 || !val) return HSPMV_OK;
-  const int64_t nnz = rp[m];
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device) != hipSuccess ||
       cus <= 0)
@@ -997,17 +996,39 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     lcs.push_back((int32_t)slice_k.size());
   }
   const int64_t n_slices = (int64_t)slice_k.size();
-  // row blocks, nnz-balanced over the regular rows, capped in rows
+  // Row blocks PER COLUMN PART.  Part h is a fixed slice of x,
+  // [ceil(n h / H), ceil(n (h + 1) / H)), and workgroup j works on part
+  // j % H: under round-robin dispatch (workgroup j on XCD j % 8;
+  // tools/xcd_map_probe.hip records it per box) every XCD sweeps one slice,
+  // which its 4 MiB L2 keeps for all its CUs.  Each part has its OWN row
+  // partition, balanced on the nonzeros that fall in that part and capped in
+  // rows (the LDS slots), so the parts' workgroups carry equal work whatever
+  // the ordering: with one row partition for all parts an RCM-ordered
+  // power-law matrix put ~90 % of a block's entries in one part (322 us vs
+  // 108 us on the same matrix unordered), and quantile splits per block, which
+  // balance the work but let every XCD sweep all of x, still took 205 us.
   const int64_t nb0 = std::max<int64_t>(1, (int64_t)cus * bpc / H);
   const int64_t reserve = n_slices / nb0 + 2;
   const int64_t row_cap = max_slots - 1 - reserve;
   if (row_cap < 64) return HSPMV_OK;  // too many slices for the LDS: not this path
-  // Greedy cuts at `target` nonzeros or row_cap rows.  The target is the
-  // smallest that yields at most nb0 blocks: one more block than CUs per part
-  // would run a second round of workgroups on two CUs and double the launch
-  // (an RCM-ordered power-law matrix, whose sparse ends hit the row cap, got
-  // 129 blocks at the mean target: 291 vs 108 us).
-  auto cut = [&](int64_t target, std::vector<int32_t> *out) -> int64_t {
+  std::vector<int32_t> cnt((size_t)(H * m), 0);  // [h][r]: row r's in-kernel nonzeros in part h
+  {
+    const int ntc = (int)std::max<int64_t>(1, std::min<int64_t>(16, m / 65536));
+    std::vector<std::thread> th;
+    for (int t = 0; t < ntc; ++t)
+      th.emplace_back([&, t]() {
+        for (int64_t r = m * t / ntc; r < m * (t + 1) / ntc; ++r) {
+          if (rp[r + 1] - rp[r] > long_t) continue;
+          for (int32_t k = rp[r]; k < rp[r + 1]; ++k) ++cnt[(size_t)(part_of(col[k]) * m + r)];
+        }
+      });
+    for (auto &x : th) x.join();
+  }
+  // Greedy cuts at `target` nonzeros or row_cap rows; the target is the
+  // smallest that yields at most nb0 blocks (one block more would run a
+  // second round of workgroups on one CU and double the launch).
+  auto cut = [&](int h, int64_t target, std::vector<int32_t> *out) -> int64_t {
+    const int32_t *c = cnt.data() + (size_t)h * (size_t)m;
     int64_t start = 0, acc = 0, nblk = 1;
     if (out) out->assign(1, 0);
     for (int64_t r = 0; r < m; ++r) {
@@ -1017,33 +1038,49 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
         start = r;
         acc = 0;
       }
-      const int64_t d = rp[r + 1] - rp[r];
-      acc += d > long_t ? 0 : d;
+      acc += c[r];
     }
     if (out) out->push_back((int32_t)m);
     return nblk;
   };
-  int64_t lo = std::max<int64_t>(1, (nnz - long_nnz + nb0 - 1) / nb0), hi = std::max<int64_t>(lo, nnz + 1);
-  if (cut(lo, nullptr) > nb0) {
-    if (cut(hi, nullptr) > nb0) lo = hi;  // the row cap alone needs more blocks
-    while (lo < hi) {
-      const int64_t mid = lo + (hi - lo) / 2;
-      if (cut(mid, nullptr) <= nb0) hi = mid; else lo = mid + 1;
+  std::vector<std::vector<int32_t>> brh((size_t)H);
+  int64_t NB = 0;
+  for (int h = 0; h < H; ++h) {
+    int64_t tot_h = 0;
+    for (int64_t r = 0; r < m; ++r) tot_h += cnt[(size_t)(h * m + r)];
+    int64_t lo = std::max<int64_t>(1, (tot_h + nb0 - 1) / nb0), hi = std::max<int64_t>(lo, tot_h + 1);
+    if (cut(h, lo, nullptr) > nb0) {
+      if (cut(h, hi, nullptr) > nb0) lo = hi;  // the row cap alone needs more blocks
+      while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (cut(h, mid, nullptr) <= nb0) hi = mid; else lo = mid + 1;
+      }
     }
+    cut(h, lo, &brh[(size_t)h]);
+    NB = std::max<int64_t>(NB, (int64_t)brh[(size_t)h].size() - 1);
   }
-  std::vector<int32_t> br;
-  cut(lo, &br);
-  const int64_t NB = (int64_t)br.size() - 1;
+  std::vector<int32_t>().swap(cnt);
   const int64_t G = NB * H;
   if (G >= INT32_MAX) return HSPMV_OK;
+  // workgroup j: part j % H, that part's block j / H (empty past its blocks)
+  std::vector<int32_t> wg_rows((size_t)(2 * G), (int32_t)m);
+  for (int64_t j = 0; j < G; ++j) {
+    const auto &b = brh[(size_t)(j % H)];
+    const int64_t i = j / H;
+    if (i + 1 < (int64_t)b.size()) {
+      wg_rows[(size_t)(2 * j)] = b[(size_t)i];
+      wg_rows[(size_t)(2 * j + 1)] = b[(size_t)i + 1];
+    }
+  }
   // slices dealt round-robin over the blocks of their part
   std::vector<std::vector<int32_t>> wg_sl((size_t)G);
   {
     std::vector<int64_t> next((size_t)H, 0);
     for (int64_t sl = 0; sl < n_slices; ++sl) {
       const int h = slice_part[(size_t)sl];
-      const int64_t rb = next[(size_t)h]++ % NB;
-      wg_sl[(size_t)(rb * H + h)].push_back((int32_t)sl);
+      const int64_t nbh = (int64_t)brh[(size_t)h].size() - 1;
+      const int64_t i = next[(size_t)h]++ % nbh;
+      wg_sl[(size_t)(i * H + h)].push_back((int32_t)sl);
     }
   }
   // per workgroup: sorted entries, chunk count (pass 1)
@@ -1054,26 +1091,25 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   std::atomic<bool> too_big{false};
   auto chunk_walk = [&](const std::vector<CsEnt> &E, auto &&emit) {
     // chunks of C entries, closed early when the span would pass 65535
-    int64_t i = 0, cnt = 0;
+    int64_t i = 0, cnt_ = 0;
     const int64_t ne = (int64_t)E.size();
     while (i < ne) {
       const uint32_t c0 = E[(size_t)i].col;
       int64_t j = i;
       while (j < ne && j - i < C && E[(size_t)j].col - c0 <= 65535u) ++j;
-      emit(cnt, c0, i, j);
-      ++cnt;
+      emit(cnt_, c0, i, j);
+      ++cnt_;
       i = j;
     }
-    return cnt;
+    return cnt_;
   };
   {
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t)
       th.emplace_back([&, t]() {
         for (int64_t b = t; b < G; b += nt) {
-          const int64_t rb = b / H;
           const int h = (int)(b % H);
-          const int32_t r0 = br[(size_t)rb], r1 = br[(size_t)rb + 1];
+          const int32_t r0 = wg_rows[(size_t)(2 * b)], r1 = wg_rows[(size_t)(2 * b + 1)];
           const int32_t nr = r1 - r0;
           auto &E = ents[(size_t)b];
           for (int32_t r = r0; r < r1; ++r) {
@@ -1177,8 +1213,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     if (!h.empty()) HIP_TRY(hipMemcpy(*d, h.data(), sizeof(E) * h.size(), hipMemcpyHostToDevice));
     return HSPMV_OK;
   };
-  if ((rc = up(&s.d_cs_blk_c, blk_c)) || (rc = up(&s.d_cs_blk_r, br)) || (rc = up(&s.d_cs_blk_v, blk_v)) ||
-      (rc = up(&s.d_cs_vslice, vslice)) || (rc = up(&s.d_cs_cbase, cbase)))
+  if ((rc = up(&s.d_cs_blk_c, blk_c)) || (rc = up(&s.d_cs_blk_r, wg_rows)) ||
+      (rc = up(&s.d_cs_blk_v, blk_v)) || (rc = up(&s.d_cs_vslice, vslice)) || (rc = up(&s.d_cs_cbase, cbase)))
     return rc;
   if (dtype == HSPMV_F32) {
     uint64_t *d = nullptr;
@@ -1222,6 +1258,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.blk_c = s.d_cs_blk_c;
   c.blk_r = s.d_cs_blk_r;
   c.blk_v = s.d_cs_blk_v;
+  c.row_blocks = (int32_t)NB;
   c.vslice = s.d_cs_vslice;
   c.cbase = s.d_cs_cbase;
   c.ent = s.d_cs_ent;
@@ -2218,6 +2255,7 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
                    : s.h_tasks.empty() ? HSPMV_CSR3_PLAN_SSR
                    : csr3_fill(s.tune) ? HSPMV_CSR3_PLAN_ALIGNED : HSPMV_CSR3_PLAN_PACKED;
   out->csort_slot_bytes = s.plan.kernel == kCsort ? (s.dp.cs.slot32 ? 4 : 8) : 0;
+  out->csort_row_blocks = s.plan.kernel == kCsort ? s.dp.cs.row_blocks : 0;
   return HSPMV_OK;
 }
 

@@ -79,11 +79,11 @@ enum Kernel : int { kAuto = 0, kVector = 1, kStream = 2, kCsr3 = 3, kCsort = 4 }
 constexpr int32_t kLongRow = 4096;
 constexpr int32_t kLongChunk = 4096;
 
-// Column-sorted row blocks (csort.hip): workgroup b = (row block b / H,
-// column part b % H) walks chunks [blk_c[b], blk_c[b+1]) of 64*u entries in
-// column order; its rows are [blk_r[b/H], blk_r[b/H+1]) and its long-row
-// slices vslice[blk_v[b] .. blk_v[b+1]).  Built by build_csort
-// (hspmv_api.cpp).
+// Column-sorted row blocks (csort.hip): workgroup b works on column part
+// b % H (a fixed slice of x) and walks chunks [blk_c[b], blk_c[b+1]) of 64*u
+// entries in column order; its rows are [blk_r[2b], blk_r[2b+1]) (each part
+// has its own row partition) and its long-row slices vslice[blk_v[b] ..
+// blk_v[b+1]).  Built by build_csort (hspmv_api.cpp).
 constexpr int kCsortThreads = 1024;
 constexpr int kCsortMaxLds = 160 * 1024;
 struct DevCsort {
@@ -95,6 +95,7 @@ struct DevCsort {
   int64_t m = 0;
   int32_t lds_bytes = 0;
   const int32_t *blk_c = nullptr, *blk_r = nullptr, *blk_v = nullptr, *vslice = nullptr;
+  int32_t row_blocks = 0;  // blocks per column part (the parts' own row partitions)
   const int32_t *cbase = nullptr;
   const void *ent = nullptr;  // fp32: {idx, val} records; fp64: idx
   const void *val = nullptr;  // fp64 values (nullptr for fp32)

@@ -116,7 +116,7 @@ class Info(C.Structure):
                 ("placement_trials", C.c_int32), ("placement_pick", C.c_int32),
                 ("placement_us", C.c_double * 8),
                 ("deterministic", C.c_int32), ("csr3_plan", C.c_int32),
-                ("csort_slot_bytes", C.c_int32), ("reserved", C.c_int32)]
+                ("csort_slot_bytes", C.c_int32), ("csort_row_blocks", C.c_int32)]
 
 
 CSR3_PLANS = {"auto": 0, "aligned": 1, "packed": 2, "ssr": 3}

@@ -229,6 +229,64 @@ def gather_y(y_local, splits: np.ndarray):
     return torch.cat(parts).to(y_local.device)  # on the caller's device whatever the backend
 
 
+def chunk_splits(A: CsrMatrix, k: int) -> np.ndarray:
+    """k contiguous, nnz-balanced row ranges of this rank's rows (k + 1 bounds)."""
+    return partition_rows(A.row_ptr, k).astype(np.int64)
+
+
+class OverlappedGather:
+    """The y all-gather overlapped with the SpMV (SURVEY.md §8e end-to-end
+    rate): the rank's rows are computed in K chunks, and chunk k's rows are
+    all-gathered (async collective, padded to the longest chunk k over the
+    ranks) while chunks k+1.. still compute.  Under "nccl" the collective is
+    issued on RCCL's stream after the work already enqueued on the current
+    stream, so it starts as soon as chunk k's kernel ends.
+
+    Usage per SpMV: for k: write chunk k's rows into ``buffer(k)[:rows[k]]``
+    (bind the chunk's y there), then ``start(k)``; finally ``finish()``
+    returns the full-length y (rank order, then chunk order)."""
+
+    def __init__(self, chunk_rows, device="cpu", dtype=None):
+        import torch
+        import torch.distributed as dist
+        self.world = dist.get_world_size()
+        self.k = len(chunk_rows)
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        mine = torch.tensor([int(v) for v in chunk_rows], dtype=torch.int64, device=dev)
+        allr = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(allr, mine)
+        self.rows = np.stack([r.cpu().numpy() for r in allr])       # [world][K]
+        self.pad = self.rows.max(axis=0)                             # per chunk
+        dtype = dtype or torch.float64
+        self.bufs = [torch.zeros(max(int(p), 1), dtype=dtype, device=device) for p in self.pad]
+        self.outs = [torch.empty(max(int(p), 1) * self.world, dtype=dtype, device=device)
+                     for p in self.pad]
+        self.works = [None] * self.k
+
+    def buffer(self, k: int):
+        return self.bufs[k]
+
+    def start(self, k: int) -> None:
+        import torch.distributed as dist
+        src, dst = _staged(self.bufs[k]), _staged(self.outs[k])
+        w = dist.all_gather_into_tensor(dst, src, async_op=True)
+        self.works[k] = (w, dst)
+
+    def finish(self):
+        import torch
+        parts = []
+        for k in range(self.k):
+            w, dst = self.works[k]
+            w.wait()
+            if dst is not self.outs[k]:
+                self.outs[k].copy_(dst)
+        p = [max(int(v), 1) for v in self.pad]
+        for r in range(self.world):
+            for k in range(self.k):
+                parts.append(self.outs[k][r * p[k]: r * p[k] + int(self.rows[r][k])])
+        return torch.cat(parts)
+
+
 def checksum_ok(A: CsrMatrix, x: np.ndarray, y: np.ndarray, seed: int = 99) -> tuple[bool, float]:
     """Size-independent identity w.(A x) == (A^T w).x in fp64 -- a property
     check of the GPU y that needs neither the oracle nor a second SpMV path."""

@@ -10,6 +10,7 @@ B=heterogeneous-spmv_amd/build
 T=heterogeneous-spmv_amd/tools
 L=$B/diagenv/libhspmv.so  # reads the HSPMV_* A/B knobs
 V=${2:-"$L,$L#HSPMV_CSORT_PF=1,$L#HSPMV_CSORT_U=8,$L#HSPMV_CSORT_U=8#HSPMV_CSORT_PF=1"}
+bash heterogeneous-spmv_amd/tools/host_info.sh gpurun_out/host_${TAG}.txt
 if [ -n "$LDS_PROBE" ]; then
   echo "== lds probe" && timeout -k 10 120 $B/lds_atomic_probe > gpurun_out/lds_probe_${TAG}.jsonl && cat gpurun_out/lds_probe_${TAG}.jsonl || exit 1
 fi

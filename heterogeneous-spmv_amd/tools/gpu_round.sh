@@ -7,7 +7,7 @@ set -o pipefail
 TAG=${1:-r02}; KEXPR=${2:-}
 R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/$TAG; mkdir -p $O
 export PYTHONUNBUFFERED=1
-{ lscpu; echo; nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null; python3 -c "import os; print('affinity', len(os.sched_getaffinity(0)))"; env | grep -E '^(OMP|MAX_JOBS|GPU_MAX)' ; } > $O/host.txt 2>&1
+bash heterogeneous-spmv_amd/tools/host_info.sh $O/host.txt
 echo "== pytest gpu"
 if [ -n "$KEXPR" ]; then KARGS=(-k "$KEXPR"); else KARGS=(); fi
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${KARGS[@]}" > $O/pytest_gpu.log 2>&1

@@ -1,0 +1,24 @@
+# Records the lease's host and GPU configuration into $1 (default
+# gpurun_out/host.txt): CPU topology and cgroup quota, and -- for the
+# box-to-box spread of C3's fabric traffic -- the GPU's compute and memory
+# partition modes, VRAM, clocks, PCIe/xGMI placement (read-only queries).
+O=${1:-gpurun_out/host.txt}
+mkdir -p "$(dirname "$O")"
+{
+  echo "== date"; date -u
+  echo "== lscpu"; lscpu
+  echo "== nproc / cgroup / affinity"; nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null
+  python3 -c "import os; print('affinity', len(os.sched_getaffinity(0)))"
+  env | grep -E '^(OMP|MAX_JOBS|GPU_MAX|HIP_VISIBLE|ROCR_VISIBLE|HSA_)' | sort
+  echo "== rocm-smi partitions"; timeout 60 rocm-smi --showcomputepartition --showmemorypartition 2>&1
+  echo "== rocm-smi product / bus / vram / clocks"
+  timeout 60 rocm-smi --showproductname --showbus --showmeminfo vram --showclocks --showfwinfo 2>&1 | grep -v '^$'
+  echo "== amd-smi static"; timeout 60 amd-smi static 2>&1 | head -200
+  echo "== amd-smi partition"; timeout 60 amd-smi partition 2>&1 | head -60
+  echo "== rocminfo (agent 2)"; timeout 60 rocminfo 2>&1 | grep -E 'Marketing|Compute Unit|Max Clock|Size:|Segment|L2|Cacheline' | head -40
+} > "$O" 2>&1
+echo "host info -> $O"
+B=$(dirname "$0")/../build
+if [ -x $B/xcd_map_probe ]; then
+  { echo "== workgroup -> XCD mapping (tools/xcd_map_probe.hip)"; timeout -k 5 60 $B/xcd_map_probe 2048 256; timeout -k 5 60 $B/xcd_map_probe 256 1024; } >> "$O" 2>&1
+fi

@@ -158,7 +158,8 @@ typedef struct {
   int32_t csr3_plan;        /* CSR3 kernel: the HSPMV_CSR3_PLAN_* it runs;
                                0 for the other kernels                      */
   int32_t csort_slot_bytes; /* CSORT: LDS row-slot width (8 = fp64 sums)    */
-  int32_t reserved;
+  int32_t csort_row_blocks; /* CSORT: row blocks per column part (each part
+                               has its own nnz-balanced row partition)     */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;

@@ -90,8 +90,16 @@ def test_bench_json_line_contract():
     assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert r["kernel"].startswith("hspmv_csr3<double")
     assert r["launches_per_spmv"] == 1 and r["csort_parts"] == 0
+    assert d["config"]["csr3_plan"] == "aligned" and d["config"]["deterministic"] is True
+    plans = d["csr3_maps_plans"]  # the maps-driven plans, same process, same y bits
+    for p, code in (("packed", 2), ("ssr", 3)):
+        assert plans[p]["csr3_plan"] == code and plans[p]["launch_us_events"] > 0
+        assert plans[p]["y_bitwise_equal_to_headline"] is True
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
+    # the reported leg runs within the cgroup quota: TimeAvg close to TimeMin
+    if c["cgroup_cpu_quota"]:
+        assert c["cores"] <= c["cgroup_cpu_quota"]
     assert abs(c["value"] - 2 * d["config"]["nnz"] / c["time_min_s"] * 1e-9) < 1e-2 * c["value"]
     assert "nnz=51895117" in c["sample"]
     ref = c["reference_f32"]  # the reference's own omp_spmv, when oracle/_ref was built
@@ -101,6 +109,7 @@ def test_bench_json_line_contract():
     assert d["check"]["pass"] is True
     sr = d["scaling_reference"]  # C4 on this one GPU: the N = 1 point of the N > 1 curve
     assert sr["config"].startswith("c4") and sr["nnz"] > 199_999_000 and sr["value"] > 0
+    assert sr["check"]["pass"] is True
 
 
 @pytest.mark.gpu
@@ -131,5 +140,7 @@ def test_bench_multi_rank_path_rehearsal_on_one_gpu(tmp_path):
     c = d["comm"]
     assert c["bcast_x_ms"] > 0 and c["gather_y_ms"] > 0 and c["halo_x_ms"] > 0
     assert c["halo_bytes_per_rank"] == 1000 * 8   # one grid line from the neighbour
+    ov = c["overlap"]  # chunked SpMV with the y all-gather overlapped
+    assert ov["chunks"] == 4 and ov["ms"] > 0 and ov["y_equal_to_plain_gather"] is True
     assert d["cpu_baseline"] is None              # rank 0 at N = 1 only
     assert d["scaling_reference"] is None

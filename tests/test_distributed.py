@@ -164,3 +164,53 @@ def test_halo_exchange_replaces_x_broadcast_gloo(world):
         peers = [p for p, _, _ in recvs]
         assert peers == [r for r in (rank - 1, rank + 1) if 0 <= r < world]
         assert nbytes == 64 * 8 * len(peers)
+
+
+def _overlap_worker(rank, world, port, K, q):
+    sys.path.insert(0, str(REPO / "heterogeneous-spmv_amd"))
+    sys.path.insert(0, str(REPO / "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from hspmv import dist as hdist
+        from hspmv import gen
+        sh = hdist.build_shard("small", rank, world)
+        xg = gen.rand_x(sh.n_global, 42)
+        sub = hdist.chunk_splits(sh.A, K)
+        og = hdist.OverlappedGather(np.diff(sub))
+        for k in range(K):  # chunk k computed (the GPU's stand-in), then its gather starts
+            a, b = int(sub[k]), int(sub[k + 1])
+            Ak = sh.A.rows(a, b)
+            og.buffer(k)[: b - a] = torch.from_numpy(oracle.spmv(Ak.row_ptr, Ak.col_idx, Ak.val, xg))
+            og.start(k)
+        y = og.finish().numpy()
+        q.put((rank, y, [int(v) for v in np.diff(sub)]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,K", [(2, 4), (3, 3), (2, 1)])
+def test_overlapped_chunked_gather_gloo(world, K):
+    """The y all-gather overlapped with the SpMV (bench.py comm
+    end_to_end_overlapped_gflops): each rank's rows in K nnz-balanced chunks,
+    chunk k gathered (async, padded per chunk) as soon as it is written; the
+    assembled y equals the oracle on the global matrix on every rank."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle
+    from hspmv import gen
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, K, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    A = gen.laplace2d(64, 64 * world)
+    y_ref = oracle.spmv(A.row_ptr, A.col_idx, A.val, gen.rand_x(A.n, 42))
+    for rank, y, rows in res:
+        assert len(rows) == K and sum(rows) > 0
+        assert np.array_equal(y, y_ref), rank

@@ -104,3 +104,4 @@ def test_bench_nccl_two_ranks():
     assert d["check"]["pass"] is True and d["scaling"] == "strong"
     c = d["comm"]
     assert c["bcast_x_ms"] > 0 and c["gather_y_ms"] > 0 and c["halo_x_ms"] > 0
+    assert c["overlap"]["y_equal_to_plain_gather"] is True
