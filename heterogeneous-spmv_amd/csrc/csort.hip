@@ -117,11 +117,17 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     const int32_t *__restrict__ blk_r, const int32_t *__restrict__ blk_v,
     const int32_t *__restrict__ vslice, const int32_t *__restrict__ cbase,
     const void *__restrict__ ent, const T *__restrict__ val, const T *__restrict__ x,
-    S *__restrict__ part, S *__restrict__ spart, T *__restrict__ y) {
+    S *__restrict__ part, S *__restrict__ spart, T *__restrict__ y,
+    unsigned long long *__restrict__ trace) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   S *acc = reinterpret_cast<S *>(smem);
   constexpr int NW = kCsortThreads / kWave;
   const int b = blockIdx.x;
+  if (trace && threadIdx.x == 0) {  // diagnostic builds only (DevCsort.trace)
+    trace[3 * b] = __builtin_amdgcn_s_memrealtime();
+    trace[3 * b + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 20) |
+                       ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32);
+  }
   const int h = b % H;  // the column part; its rows: the part's own row block
   const int32_t c0 = blk_c[b], c1 = blk_c[b + 1];
   const int32_t r0 = blk_r[2 * b], r1 = blk_r[2 * b + 1];
@@ -137,7 +143,10 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   if constexpr (PF)
     if (c0 + wid < c1) load_entries<T, U, NT, WIDE>(ent, val, c0 + wid, lane, ix, vv);
   for (int32_t c = c0 + wid; c < c1; c += NW) {  // wave-uniform
-    const int32_t base = wave_uniform(cbase[wave_uniform(c)]);
+    // bit 31 of the chunk base: a "segmented" chunk (see below)
+    const uint32_t cb = (uint32_t)wave_uniform(cbase[wave_uniform(c)]);
+    const int32_t base = (int32_t)(cb & 0x7fffffffu);
+    const bool seg = (cb >> 31) != 0u;
     if constexpr (!PF) load_entries<T, U, NT, WIDE>(ent, val, c, lane, ix, vv);
     T xv[U];
 #pragma unroll
@@ -154,17 +163,44 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
       if (c + NW < c1) load_entries<T, U, NT, WIDE>(ent, val, c + NW, lane, ix, vv);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (!seg) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      S pr;
-      if constexpr (sizeof(T) == 4 && sizeof(S) == 8)
-        pr = (double)vvc[u] * (double)xv[u];  // exact
-      else
-        pr = (S)(vvc[u] * xv[u]);  // omp_spmv's rounded product
-      atomicAdd(&acc[ixc[u] >> 16], pr);
+      for (int u = 0; u < U; ++u) {
+        S pr;
+        if constexpr (sizeof(T) == 4 && sizeof(S) == 8)
+          pr = (double)vvc[u] * (double)xv[u];  // exact
+        else
+          pr = (S)(vvc[u] * xv[u]);  // omp_spmv's rounded product
+        atomicAdd(&acc[ixc[u] >> 16], pr);
+      }
+    } else {
+      // Segmented chunk: the host found rows whose entries crowd one
+      // instruction (a hub row's contiguous columns after an RCM ordering:
+      // up to 64 lanes on one slot, and same-address LDS atomics serialise)
+      // and stored the chunk sorted by slot.  Each instruction's lanes of
+      // one slot are summed first (segmented scan over the sorted slots),
+      // and the last lane of each run adds it: one atomic per row run.
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        S v;
+        if constexpr (sizeof(T) == 4 && sizeof(S) == 8)
+          v = (double)vvc[u] * (double)xv[u];
+        else
+          v = (S)(vvc[u] * xv[u]);
+        const uint32_t sl = ixc[u] >> 16;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+          const S ov = __shfl_up(v, off, kWave);
+          const uint32_t os = __shfl_up(sl, off, kWave);
+          if (lane >= off && os == sl) v += ov;
+        }
+        const uint32_t ns = __shfl_down(sl, 1, kWave);
+        if (lane == kWave - 1 || ns != sl) atomicAdd(&acc[sl], v);
+      }
     }
   }
   __syncthreads();
+  if (trace && threadIdx.x == 0) trace[3 * b + 1] = __builtin_amdgcn_s_memrealtime();
   if (direct) {  // one column part, no long rows: y straight from the slots
     for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) y[r0 + i] = (T)acc[i];
     return;
@@ -231,7 +267,8 @@ template <typename T, typename S, int U, bool NT, bool PF, bool WIDE>
 void launch_csort_main(const DevCsort &c, const T *x, S *part, S *spart, T *y, hipStream_t st) {
   hipLaunchKernelGGL((hspmv_csort<T, S, U, NT, PF, WIDE>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
                      (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
-                     c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y);
+                     c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y,
+                     c.trace);
 }
 
 template <typename T, typename S, int U, bool NT>

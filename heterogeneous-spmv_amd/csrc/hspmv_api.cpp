@@ -66,6 +66,7 @@ struct Shard {
           *d_cs_vslice = nullptr, *d_cs_cbase = nullptr, *d_cs_long_row = nullptr,
           *d_cs_long_cs = nullptr;
   uint32_t *d_cs_mask = nullptr;
+  unsigned long long *d_cs_trace = nullptr;  // diagnostic builds: csort per-workgroup timestamps
   void *d_cs_ent = nullptr, *d_cs_val = nullptr;
   double *d_cs_part = nullptr, *d_cs_spart = nullptr;
   DevCsort csort;
@@ -182,6 +183,10 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_CSORT_BPC", &t->csort_blocks_per_cu);
   geti("HSPMV_CSORT_SLOT32", &t->csort_slot32);
   geti("HSPMV_CSORT_WIDE", &t->csort_wide);
+  geti("HSPMV_CSORT_LDS", &t->csort_lds_cap);
+  geti("HSPMV_CSORT_SEG", &t->csort_seg);
+  geti("HSPMV_CSORT_SEG_EXTRA", &t->csort_seg_extra);
+  geti("HSPMV_CSORT_TRACE", &t->csort_trace);
   geti("HSPMV_STREAM_W", &t->stream_waves);
   geti("HSPMV_PLACEMENT", &t->placement_trials);
   geti("HSPMV_CONTIG", &t->contig);
@@ -239,7 +244,7 @@ void free_shard(Shard &s, bool borrowed) {
   for (void *p : {(void *)s.d_cs_blk_c, (void *)s.d_cs_blk_r, (void *)s.d_cs_blk_v,
                   (void *)s.d_cs_vslice, (void *)s.d_cs_cbase, (void *)s.d_cs_long_row,
                   (void *)s.d_cs_long_cs, (void *)s.d_cs_mask, s.d_cs_ent, s.d_cs_val,
-                  (void *)s.d_cs_part, (void *)s.d_cs_spart})
+                  (void *)s.d_cs_part, (void *)s.d_cs_spart, (void *)s.d_cs_trace})
     (void)hipFree(p);
   (void)hipFree(s.d_task);
   (void)hipFree(s.d_long_row);
@@ -939,6 +944,9 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
 // Tuning.csort_parts = 1/2/4 sets the column parts, csort_u = 4/8/16 the
 // chunk.  The row blocks are capped by the device's LDS per workgroup.
 constexpr int32_t kCsortSlice = 2048;
+// a chunk whose instructions would serialise more than this many same-slot
+// lanes in all is stored slot-sorted (segmented)
+constexpr int64_t kCsortSegExtra = 512;
 
 struct CsEnt {
   uint32_t col, slot, k;
@@ -960,6 +968,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     return HSPMV_OK;
   lds_max = std::min(lds_max, kCsortMaxLds);
   const Tuning &tn = s.tune;
+  if (tn.csort_lds_cap > 0) lds_max = std::min(lds_max, tn.csort_lds_cap);  // A/B
   const bool slot32 = dtype == HSPMV_F32 && tn.csort_slot32 == 1;
   const int64_t slot_bytes = slot32 ? 4 : 8;
   const int32_t max_slots = (int32_t)(lds_max / slot_bytes) - 1;
@@ -1171,16 +1180,50 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
             const int64_t u = q / 64, lane = q % 64;
             return (u / per) * (64 * per) + lane * per + (u % per);
           };
+          std::vector<CsEnt> tmp;
+          uint32_t sl64[64];
           chunk_walk(E, [&](int64_t ci, uint32_t c0, int64_t i, int64_t j) {
             const int64_t ch = cfirst + ci;
-            cbase[(size_t)ch] = (int32_t)c0;
+            // Same-slot lanes in one instruction serialise the LDS atomics:
+            // an RCM ordering puts a hub row's entries on contiguous columns,
+            // so column order can give one instruction 64 lanes of one row
+            // (RCM power-law: a few workgroups with ~100 K serialised lanes
+            // set the launch's tail, 204 vs 108 us).  Such chunks are stored
+            // sorted by slot instead and flagged (bit 31 of the base): the
+            // kernel sums each instruction's runs first (segmented scan).
+            const CsEnt *src = E.data() + i;
+            bool seg = false;
+            if (tn.csort_seg != 0) {
+              int64_t extra = 0;
+              for (int64_t g = i; g < j; g += 64) {
+                const int64_t e = std::min(j, g + 64);
+                for (int64_t t = g; t < e; ++t) sl64[t - g] = E[(size_t)t].slot;
+                std::sort(sl64, sl64 + (e - g));
+                int run = 1, mx = 1;
+                for (int64_t t = 1; t < e - g; ++t) {
+                  run = sl64[t] == sl64[t - 1] ? run + 1 : 1;
+                  mx = std::max(mx, run);
+                }
+                extra += mx - 1;
+              }
+              const int64_t lim = tn.csort_seg_extra > 0 ? tn.csort_seg_extra : kCsortSegExtra;
+              if (extra > lim || tn.csort_seg == 2) {
+                tmp.assign(E.begin() + i, E.begin() + j);
+                std::sort(tmp.begin(), tmp.end(), [](const CsEnt &a, const CsEnt &b) {
+                  return a.slot != b.slot ? a.slot < b.slot : (a.col != b.col ? a.col < b.col : a.k < b.k);
+                });
+                src = tmp.data();
+                seg = true;
+              }
+            }
+            cbase[(size_t)ch] = (int32_t)(c0 | (seg ? 0x80000000u : 0u));
             for (int64_t q = 0; q < C; ++q) {
               const int64_t o = ch * C + at(q, dtype == HSPMV_F32 ? 2 : 4);
               const int64_t ov = ch * C + at(q, 2);
               uint32_t ix = dummy << 16;  // padding: 0 * x[base] into the dummy slot
               const void *vp = nullptr;
               if (i + q < j) {
-                const CsEnt &e = E[(size_t)(i + q)];
+                const CsEnt &e = src[q];
                 ix = (e.slot << 16) | (e.col - c0);
                 vp = (const char *)val + sv * (size_t)e.k;
               }
@@ -1259,6 +1302,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.blk_r = s.d_cs_blk_r;
   c.blk_v = s.d_cs_blk_v;
   c.row_blocks = (int32_t)NB;
+  if (tn.csort_trace == 1 && (rc = dev_alloc(&s.d_cs_trace, 24 * (size_t)G, &s.bytes))) return rc;
+  c.trace = s.d_cs_trace;
   c.vslice = s.d_cs_vslice;
   c.cbase = s.d_cs_cbase;
   c.ent = s.d_cs_ent;
@@ -2258,6 +2303,23 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   out->csort_row_blocks = s.plan.kernel == kCsort ? s.dp.cs.row_blocks : 0;
   return HSPMV_OK;
 }
+
+#ifdef HSPMV_ENV_KNOBS
+// Diagnostic builds only (not in hspmv.h): the last csort launch's
+// per-workgroup {start, end, XCC_ID | HW_ID << 32} (s_memrealtime ticks),
+// when the handle was created with HSPMV_CSORT_TRACE=1.  Returns the
+// workgroup count (0: no trace).
+int hspmv_diag_csort_trace(hspmv_handle *h, unsigned long long *out, int max_wg) {
+  if (!h || h->shards.empty()) return 0;
+  const Shard &s = h->shards[0];
+  if (s.plan.kernel != kCsort || !s.dp.cs.trace) return 0;
+  const int n = std::min(max_wg, s.dp.cs.n_wg);
+  if (hipSetDevice(s.device) != hipSuccess || hipStreamSynchronize(s.stream) != hipSuccess ||
+      hipMemcpy(out, s.dp.cs.trace, 24 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return n;
+}
+#endif
 
 int hspmv_get_info_sized(hspmv_handle *h, hspmv_info *out, uint32_t out_size) {
   clear_error();

@@ -64,6 +64,10 @@ struct Tuning {
   int csort_blocks_per_cu = 0;           // row blocks per CU and part (0: 1)
   int csort_slot32 = -1;                 // fp32 LDS row slots (fp32 data)
   int csort_wide = -1;                   // 16-byte entry loads (interleaved layout)
+  int csort_lds_cap = 0;                 // LDS bytes per workgroup for the row slots (0: all)
+  int csort_seg = -1;                    // segmented chunks: 0 never, 2 always (-1: by conflicts)
+  int csort_seg_extra = 0;               // serialised same-slot lanes that flag a chunk (0: default)
+  int csort_trace = 0;                   // per-workgroup timestamps (hspmv_diag_csort_trace)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
 };
@@ -96,6 +100,7 @@ struct DevCsort {
   int32_t lds_bytes = 0;
   const int32_t *blk_c = nullptr, *blk_r = nullptr, *blk_v = nullptr, *vslice = nullptr;
   int32_t row_blocks = 0;  // blocks per column part (the parts' own row partitions)
+  unsigned long long *trace = nullptr;  // diagnostic builds: per-workgroup {start, end, hw_id} (s_memrealtime)
   const int32_t *cbase = nullptr;
   const void *ent = nullptr;  // fp32: {idx, val} records; fp64: idx
   const void *val = nullptr;  // fp64 values (nullptr for fp32)

@@ -160,6 +160,44 @@ def test_csort_run_to_run_fp64_and_deterministic_option():
         hspmv.SpMV(A, kernel="csort", options={"deterministic": 1})
 
 
+def _hub_rows(seed=5, m=40_000, n=400_000):
+    """Random short rows plus hub rows whose 1000-4000 columns are
+    CONTIGUOUS (what an RCM ordering does to a power-law graph's hubs): in
+    column order their entries fill whole instructions with one row, so the
+    builder stores those chunks slot-sorted and the kernel pre-sums each
+    row's lanes (segmented chunks)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 30, m)
+    hubs = rng.choice(m, 12, replace=False)
+    lens[hubs] = rng.integers(1000, 4000, hubs.size)
+    cols = []
+    for r, ln in enumerate(lens):
+        if r in set(hubs.tolist()):
+            c0 = int(rng.integers(0, n - ln))
+            cols.append(np.arange(c0, c0 + ln))
+        else:
+            cols.append(np.sort(rng.choice(n, ln, replace=False)))
+    rp = np.concatenate([[0], np.cumsum(lens)])
+    return hspmv.CsrMatrix(m, n, rp, np.concatenate(cols), rng.uniform(-1, 1, rp[-1]))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_csort_segmented_chunks_for_contiguous_hub_rows(dtype):
+    A = _hub_rows().astype(dtype)
+    x = gen.rand_x(A.n, 12).astype(dtype)
+    for parts in (1, 2):
+        y, info = run(A, x, kernel="csort", options={"csort_parts": parts})
+        assert info["kernel_name"] == "csort" and info["csort_row_blocks"] > 0
+        check(A, x, y)
+
+
+def test_csort_rcm_powerlaw_matches_oracle():
+    A = gen.powerlaw(150_000, seed=21, dtype=np.float32, rcm=True)
+    x = gen.rand_x(A.n, 4).astype(np.float32)
+    y, info = run(A, x, kernel="csort")
+    check(A, x, y)
+
+
 def test_csort_padding_does_not_spread_inf():
     A = gen.powerlaw(30_000, seed=6, dtype=np.float64)
     x = gen.rand_x(A.n, 5)

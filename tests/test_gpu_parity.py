@@ -326,6 +326,31 @@ def test_config_c5_powerlaw_csr3_fp32():
     assert np.array_equal(ys[ok].view(np.uint32), y32[ok].view(np.uint32))
 
 
+def test_config_c5r_powerlaw_rcm_csr3_fp32():
+    """C5's matrix in the reference's input ordering: RCM-permuted
+    (helpers/converter.m:8,14, symrcm -> .mtx.rcm.csr).  RCM leaves a
+    random graph's columns scattered, so AUTO still takes the column-sorted
+    kernel (per-part row partitions keep its column parts balanced; hub
+    rows' contiguous columns go to segmented chunks); checked like C5."""
+    A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32, rcm=True)
+    maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
+    x = gen.rand_x(A.n, 9).astype(np.float32)
+    y, info = gpu_spmv(A, x, maps)
+    lens = np.diff(A.row_ptr)
+    assert info["kernel_name"] == "csort" and info["n_split_rows"] == int((lens > 4096).sum())
+    y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    assert np.all(np.abs(y - y64) <= 2.0 ** -24 * np.abs(y64) + 1e-12 * absrow)
+    y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    err = np.abs(y.astype(np.float64) - y32.astype(np.float64))
+    assert np.all(err <= (lens + 2) * 2.0 ** -23 * absrow + 1e-30)
+    # deterministic row kernels on the same matrix: bitwise on short rows
+    yd, idet = gpu_spmv(A, x, maps, options={"deterministic": 1})
+    assert idet["kernel_name"] == "csr3"
+    ok = short_rows(A)
+    assert np.array_equal(yd[ok].view(np.uint32), y32[ok].view(np.uint32))
+
+
 def _split_row_matrix(seed=3):
     """Rows of 5e3 .. 1.2e5 nonzeros (split rows) beside short and medium rows,
     including split rows first, last, adjacent, and at 64-row group edges."""
