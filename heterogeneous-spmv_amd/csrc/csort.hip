@@ -53,6 +53,48 @@ __device__ __forceinline__ int32_t wave_uniform(int32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+// One DPP move (both dwords for fp64); lanes the pattern does not feed read
+// `old` (keys: a sentinel no slot equals; values: 0).
+template <int CTRL, int ROW_MASK, typename S>
+__device__ __forceinline__ S dpp_val(S v) {
+  if constexpr (sizeof(S) == 8) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROW_MASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+    return __builtin_bit_cast(S, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  } else {
+    return __builtin_bit_cast(S, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                             ROW_MASK, 0xf, false));
+  }
+}
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_key(uint32_t k) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)k, CTRL, ROW_MASK, 0xf, false);
+}
+
+// Inclusive segmented scan over the wave's 64 lanes; k = the lane's run id,
+// non-decreasing along the lanes (so k[l - d] == k[l] means lanes l-d .. l
+// are one run): row_shr 1/2/4/8 inside the 16-lane rows, then row_bcast
+// 15 / 31 across them.
+template <typename S>
+__device__ __forceinline__ S seg_scan(S v, uint32_t k) {
+#define HSPMV_SEG_STEP(CTRL, MASK)                        \
+  {                                                      \
+    const uint32_t kp = dpp_key<CTRL, MASK>(k);          \
+    const S vp = dpp_val<CTRL, MASK>(v);                 \
+    v += kp == k ? vp : S(0);                            \
+  }
+  HSPMV_SEG_STEP(0x111, 0xf)
+  HSPMV_SEG_STEP(0x112, 0xf)
+  HSPMV_SEG_STEP(0x114, 0xf)
+  HSPMV_SEG_STEP(0x118, 0xf)
+  HSPMV_SEG_STEP(0x142, 0xa)
+  HSPMV_SEG_STEP(0x143, 0xc)
+#undef HSPMV_SEG_STEP
+  return v;
+}
+
 // Loads chunk c's U entries per lane (idx, value): entry u of the lane is
 // the chunk's sorted entry u*64 + lane.  WIDE: 16-byte loads over a layout
 // interleaved on the host (build_csort) so that one load brings the lane
@@ -177,9 +219,11 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
       // Segmented chunk: the host found rows whose entries crowd one
       // instruction (a hub row's contiguous columns after an RCM ordering:
       // up to 64 lanes on one slot, and same-address LDS atomics serialise)
-      // and stored the chunk sorted by slot.  Each instruction's lanes of
-      // one slot are summed first (segmented scan over the sorted slots),
-      // and the last lane of each run adds it: one atomic per row run.
+      // and stored those rows' entries slot-sorted (consecutive lanes, in
+      // column order within a row), the chunk's other entries after them in
+      // column order.  Each instruction's runs of one slot are summed first
+      // (DPP segmented scan), and the last lane of a run adds it: one atomic
+      // per run.
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         S v;
@@ -188,14 +232,16 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
         else
           v = (S)(vvc[u] * xv[u]);
         const uint32_t sl = ixc[u] >> 16;
-#pragma unroll
-        for (int off = 1; off < kWave; off <<= 1) {
-          const S ov = __shfl_up(v, off, kWave);
-          const uint32_t os = __shfl_up(sl, off, kWave);
-          if (lane >= off && os == sl) v += ov;
-        }
-        const uint32_t ns = __shfl_down(sl, 1, kWave);
-        if (lane == kWave - 1 || ns != sl) atomicAdd(&acc[sl], v);
+        // runs = maximal stretches of lanes with one slot; run id = the
+        // number of run starts up to this lane (ballot + mbcnt)
+        const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)sl, 0x138, 0xf, 0xf, false);
+        const bool start = lane == 0 || prev != sl;  // (0x138: wave_shr 1)
+        const unsigned long long msk = __ballot(start);
+        const uint32_t rid = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u)) +
+                             (start ? 1u : 0u);
+        v = seg_scan(v, rid);
+        if (lane == kWave - 1 || ((msk >> (lane + 1)) & 1ull)) atomicAdd(&acc[sl], v);
       }
     }
   }

@@ -187,6 +187,7 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_CSORT_SEG", &t->csort_seg);
   geti("HSPMV_CSORT_SEG_EXTRA", &t->csort_seg_extra);
   geti("HSPMV_CSORT_TRACE", &t->csort_trace);
+  geti("HSPMV_CSORT_LONG", &t->csort_long);
   geti("HSPMV_STREAM_W", &t->stream_waves);
   geti("HSPMV_PLACEMENT", &t->placement_trials);
   geti("HSPMV_CONTIG", &t->contig);
@@ -946,7 +947,8 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
 constexpr int32_t kCsortSlice = 2048;
 // a chunk whose instructions would serialise more than this many same-slot
 // lanes in all is stored slot-sorted (segmented)
-constexpr int64_t kCsortSegExtra = 512;
+constexpr int64_t kCsortSegExtra = 128;
+constexpr int64_t kCsortSegHeavy = 8;  // entries of one row in a chunk that make it a run
 
 struct CsEnt {
   uint32_t col, slot, k;
@@ -979,10 +981,17 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   if (tn.csort_u == 4 || tn.csort_u == 8 || tn.csort_u == 16) U = tn.csort_u;
   const int bpc = tn.csort_blocks_per_cu > 0 ? std::min(tn.csort_blocks_per_cu, 8) : 1;
   // 16-byte entry loads: needs U a multiple of 2 (fp32 records) / 4 (fp64 indices)
-  const bool wide = tn.csort_wide == 1 && (dtype == HSPMV_F32 ? U % 2 == 0 : U % 4 == 0);
+  // 16-byte entry loads + the next chunk's entries loaded during this chunk's
+  // gathers: fp32 C5 107 -> 103 us, RCM'd C5 192 -> 190, in four one-process
+  // A/Bs (profiles/r03/ab_c5_wide_pf*.jsonl); fp64 keeps 8-byte loads
+  // (unmeasured).  Neither alone moves C5 (wide 108.8 vs 108.0, PF 109.4).
+  const bool wide_default = dtype == HSPMV_F32;
+  const bool wide = (tn.csort_wide >= 0 ? tn.csort_wide == 1 : wide_default) &&
+                    (dtype == HSPMV_F32 ? U % 2 == 0 : U % 4 == 0);
   const int64_t C = 64 * U;
   const size_t sv = dtype_size(dtype);
-  const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
+  const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX
+                         : (s.tune.csort_long > 0 ? s.tune.csort_long : kLongRow);
   auto part_of = [&](int64_t c) { return (int)((c * H) / n); };  // c in part floor(c*H/n)
   // long rows and their slices (per part, kCsortSlice nonzeros each)
   std::vector<int32_t> lrow, lcs(1, 0);
@@ -1208,10 +1217,28 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
               }
               const int64_t lim = tn.csort_seg_extra > 0 ? tn.csort_seg_extra : kCsortSegExtra;
               if (extra > lim || tn.csort_seg == 2) {
-                tmp.assign(E.begin() + i, E.begin() + j);
-                std::sort(tmp.begin(), tmp.end(), [](const CsEnt &a, const CsEnt &b) {
-                  return a.slot != b.slot ? a.slot < b.slot : (a.col != b.col ? a.col < b.col : a.k < b.k);
-                });
+                // the crowded rows (>= kCsortSegHeavy entries in this chunk)
+                // first, slot-sorted, in column order within each: their runs
+                // are contiguous columns (coalesced gathers); the other
+                // entries after them, still in column order
+                std::vector<std::pair<uint32_t, int32_t>> cnt_s;
+                cnt_s.reserve((size_t)(j - i));
+                for (int64_t t = i; t < j; ++t) cnt_s.push_back({E[(size_t)t].slot, 0});
+                std::sort(cnt_s.begin(), cnt_s.end());
+                std::vector<uint32_t> heavy;
+                for (size_t t = 0; t < cnt_s.size();) {
+                  size_t e = t;
+                  while (e < cnt_s.size() && cnt_s[e].first == cnt_s[t].first) ++e;
+                  if ((int64_t)(e - t) >= kCsortSegHeavy || tn.csort_seg == 2) heavy.push_back(cnt_s[t].first);
+                  t = e;
+                }
+                auto is_heavy = [&](uint32_t sl) { return std::binary_search(heavy.begin(), heavy.end(), sl); };
+                tmp.clear();
+                for (int64_t t = i; t < j; ++t)
+                  if (is_heavy(E[(size_t)t].slot)) tmp.push_back(E[(size_t)t]);
+                std::stable_sort(tmp.begin(), tmp.end(), [](const CsEnt &a, const CsEnt &b) { return a.slot < b.slot; });
+                for (int64_t t = i; t < j; ++t)
+                  if (!is_heavy(E[(size_t)t].slot)) tmp.push_back(E[(size_t)t]);
                 src = tmp.data();
                 seg = true;
               }
@@ -1293,6 +1320,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.n_long = (int32_t)lrow.size();
   c.nontemporal = true;  // the entry stream is read once; keep x in the caches
   if (tn.csort_nt >= 0) c.nontemporal = tn.csort_nt != 0;  // A/B knobs
+  c.prefetch = wide && dtype == HSPMV_F32;  // see `wide` above
   if (tn.csort_pf >= 0) c.prefetch = tn.csort_pf != 0;
   c.slot32 = slot32;
   c.wide = wide;

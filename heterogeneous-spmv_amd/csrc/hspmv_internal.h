@@ -68,6 +68,7 @@ struct Tuning {
   int csort_seg = -1;                    // segmented chunks: 0 never, 2 always (-1: by conflicts)
   int csort_seg_extra = 0;               // serialised same-slot lanes that flag a chunk (0: default)
   int csort_trace = 0;                   // per-workgroup timestamps (hspmv_diag_csort_trace)
+  int csort_long = 0;                    // rows above this many nonzeros are sliced (0: kLongRow)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
 };
