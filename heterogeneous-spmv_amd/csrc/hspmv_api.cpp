@@ -51,6 +51,7 @@ struct Shard {
   uint64_t *d_cplanes = nullptr;
   int32_t *d_xwin = nullptr;         // STREAM x windows {lo, w} per 64-row group
   int32_t *d_xd_blk = nullptr;       // block x dictionaries (build_xdict)
+  int64_t xd_cut = 0;                // CSR3 dictionary blocks cut in two (split_xd_blocks)
   int32_t *d_xd_runs = nullptr;
   int32_t xd_lds_bytes = 0;
   int xd_shape = 0;                  // 0 none, kStream (256-row blocks), kCsr3 (4 packed tasks)
@@ -192,6 +193,7 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_PLACEMENT", &t->placement_trials);
   geti("HSPMV_CONTIG", &t->contig);
   geti("HSPMV_XD_WAVES", &t->xd_waves);
+  geti("HSPMV_XD_BPC", &t->xd_blocks_per_cu);
   geti("HSPMV_PF", &t->pf);
   geti("HSPMV_YNT", &t->y_nt);
   geti("HSPMV_NT", &t->nt);
@@ -636,6 +638,7 @@ struct XdPlan {
   std::vector<int32_t> blk;  // nb + 1 record ranges
   std::vector<int32_t> rec;  // {x_start, lds_off} per run, sentinel {0, entries} per block
   std::vector<uint16_t> pos; // per nonzero: position in its block's staged x (0 for split rows)
+  std::vector<int32_t> total;  // entries per block
   int64_t entries = 0, in_kernel_nnz = 0;
   int32_t tmax = 0;
 };
@@ -682,6 +685,7 @@ bool plan_xdict(const int32_t *rp, const int32_t *col, const std::vector<int32_t
     }
   });
   if (fail) return false;
+  P.total = total;
   int64_t nrec = 0;
   P.blk.assign((size_t)nb + 1, 0);
   P.entries = 0;
@@ -757,6 +761,69 @@ int64_t xdict_cap_entries(int dtype, const Tuning &t) {
                            65536);
 }
 
+// Blocks per CU the CSR3 dictionary workgroups are sized for.  The LDS of a
+// workgroup is its product staging (W x 64 x U values) plus its dictionary,
+// allocated in 1 KiB granules (C3 fp64: 8 KiB + 18.8 KiB ran 5 workgroups per
+// CU, tools/block_trace.py).  A block whose dictionary would not fit 160 KiB
+// / kXdBlocksPerCu is cut into two half blocks (two tasks each, two empty
+// task slots): C3 cuts 40 of its 7630 blocks for 6 per CU.
+constexpr int kXdBlocksPerCu = 6;
+constexpr int64_t kLdsPerCu = 160 * 1024, kLdsGranule = 1024;
+
+int64_t xd_target_entries(int dtype, const Tuning &t) {
+  const int bpc = t.xd_blocks_per_cu > 0 ? t.xd_blocks_per_cu : kXdBlocksPerCu;
+  const int64_t sv = (int64_t)dtype_size(dtype);
+  // product staging of the chunk plan_launch picks for >= 12 nonzeros per
+  // row (pick_u: U = 4 fp64, 16 fp32), 4 waves
+  const int64_t staging = 4 * 64 * (sv == 8 ? 4 : 16) * sv + 16;
+  const int64_t per_block = (kLdsPerCu / bpc) / kLdsGranule * kLdsGranule;
+  return std::max<int64_t>(0, (per_block - staging) / sv);
+}
+
+// Cuts the 4-task blocks of `tasks` whose dictionary exceeds `target`
+// entries into two 2-task blocks padded with empty tasks.  Returns the
+// number of blocks cut.
+int64_t split_xd_blocks(std::vector<int32_t> &tasks, const std::vector<int32_t> &total,
+                        int64_t target) {
+  const int64_t nt = (int64_t)tasks.size() - 1, W = 4;
+  int64_t cut = 0;
+  std::vector<int32_t> out;
+  out.reserve(tasks.size() + 64);
+  for (int64_t b = 0; b * W < nt; ++b) {
+    const int64_t t0 = b * W, t1 = std::min(nt, t0 + W);
+    if (total[(size_t)b] > target && t1 - t0 > 2) {
+      ++cut;
+      const int32_t mid = tasks[(size_t)t0 + 2];
+      out.push_back(tasks[(size_t)t0]);
+      out.push_back(tasks[(size_t)t0 + 1]);
+      out.push_back(mid);
+      out.push_back(mid);  // two empty tasks
+      for (int64_t t = t0 + 2; t < t1; ++t) out.push_back(tasks[(size_t)t]);
+      for (int64_t t = t1 - t0 - 2; t < W; ++t) out.push_back(tasks[(size_t)t1]);
+    } else {
+      for (int64_t t = t0; t < t1; ++t) out.push_back(tasks[(size_t)t]);
+    }
+  }
+  out.push_back(tasks[(size_t)nt]);
+  if (cut) tasks.swap(out);
+  return cut;
+}
+
+// plan_xdict over the workgroups of `kern`; CSR3 task tables are first cut
+// for occupancy (split_xd_blocks), so the plan is the one the kernel runs.
+bool plan_xdict_for(const int32_t *rp, const int32_t *col, int kern, int64_t m,
+                    std::vector<int32_t> &tasks, int32_t long_t, int64_t cap, int dtype,
+                    const Tuning &tune, bool fill, XdPlan &P, int64_t *cut) {
+  *cut = 0;
+  const bool cuts = kern == kCsr3 && xd_task_waves(tune) == 4 && tune.xd_blocks_per_cu >= 0;
+  if (!plan_xdict(rp, col, xdict_blocks(kern, m, tasks, tune), long_t, cap, fill && !cuts, P))
+    return false;
+  if (!cuts) return true;
+  *cut = split_xd_blocks(tasks, P.total, xd_target_entries(dtype, tune));
+  if (*cut == 0 && !fill) return true;
+  return plan_xdict(rp, col, xdict_blocks(kern, m, tasks, tune), long_t, cap, fill, P);
+}
+
 // Auto mode also leaves banded matrices to the x windows (have_xwin: the
 // row kernel's window table qualified): on C4's shard the per-wave windows
 // need no block barrier and were 7 % faster than the dictionaries
@@ -776,10 +843,13 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
   if (mode < 0 && footprint <= kMallResident) return HSPMV_OK;
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
   XdPlan P;
-  if (!plan_xdict(rp, col, xdict_blocks(kern, m, s.h_tasks, s.tune), long_t,
-                  xdict_cap_entries(dtype, s.tune), true, P))
+  // (cuts the task table only when the dictionaries are taken)
+  std::vector<int32_t> tasks = s.h_tasks;
+  if (!plan_xdict_for(rp, col, kern, m, tasks, long_t, xdict_cap_entries(dtype, s.tune), dtype,
+                      s.tune, true, P, &s.xd_cut))
     return HSPMV_OK;
   if (mode < 0 && 2 * P.entries > P.in_kernel_nnz) return HSPMV_OK;  // too little reuse to pay
+  s.h_tasks.swap(tasks);
   int rc;
   if ((rc = dev_alloc(&s.d_c16, 2 * (size_t)std::max<int64_t>(nnz, 1), &s.bytes))) return rc;
   if ((rc = dev_alloc(&s.d_xd_blk, 4 * P.blk.size(), &s.bytes))) return rc;
@@ -2386,8 +2456,9 @@ int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, const hspm
   XdPlan P;
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
   const bool fill = blk || runs || pos;
-  if (!plan_xdict(A->row_ptr, A->col_idx, xdict_blocks(kern, A->m, tasks, tune), long_t,
-                  std::min<int64_t>(cap_entries, 65536), fill, P))
+  int64_t cut = 0;
+  if (!plan_xdict_for(A->row_ptr, A->col_idx, kern, A->m, tasks, long_t,
+                      std::min<int64_t>(cap_entries, 65536), A->dtype, tune, fill, P, &cut))
     return HSPMV_OK;  // some block exceeds the cap: no dictionary (n_blocks = 0)
   *n_blocks = (int64_t)P.blk.size() - 1;
   *n_records = (int64_t)P.blk.back();

@@ -59,6 +59,7 @@ struct Tuning {
   // A/B only (diagnostic builds)
   int contig = 0;           // hipDeviceMallocContiguous allocations
   int xd_waves = 0;         // packed CSR3 tasks per dictionary block (0: 4; 8)
+  int xd_blocks_per_cu = 0; // CSR3 dictionary blocks sized for this many per CU (0: 6; -1: no cuts)
   double xslab_bytes = 0;   // x bytes per slab (0: 2 MiB)
   int csort_nt = -1, csort_pf = -1;      // -1: the library's choice
   int csort_blocks_per_cu = 0;           // row blocks per CU and part (0: 1)

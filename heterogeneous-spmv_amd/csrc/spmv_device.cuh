@@ -12,8 +12,8 @@ namespace dev {
 
 // Ablation builds only (make diag): 1 = skip the ordered row sums, 2 = skip
 // the x gather (x[col] := 1), 3 = both; 16 = skip the x-dictionary staging
-// (and its barrier), 32 = the barrier without the staging loads.  Results
-// are wrong in those builds.
+// (and its barrier), 32 = the barrier without the staging loads, 256 = no y
+// stores (the sums kept live).  Results are wrong in those builds.
 #ifndef HSPMV_DIAG
 #define HSPMV_DIAG 0
 #endif
@@ -40,6 +40,20 @@ __device__ __forceinline__ unsigned long long diag_stamp() {
 #define HSPMV_TRACE(ts, i, v) \
   do {                        \
   } while (0)
+#endif
+// HSPMV_DIAG & 512: per-workgroup timeline of the CSR3 kernel -- slot 0 the
+// workgroup's start, 1..4 each wave's end (after its y store is issued), 6
+// HW_ID, 7 XCC_ID (s_memrealtime, 100 MHz; no waits, results correct) --
+// into g_trace[block * kTraceSlots] (tools/block_trace.py).
+#if (HSPMV_DIAG & 512)
+#if !(HSPMV_DIAG & 8)
+static __device__ unsigned long long g_trace[kTraceWaves * kTraceSlots];
+#endif
+__device__ __forceinline__ unsigned long long diag_realtime() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
 #endif
 
 constexpr int kWave = 64;
@@ -430,7 +444,9 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
 #if (HSPMV_DIAG & 8)
   HSPMV_TRACE(ts, 5, diag_stamp());
 #endif
-  if (valid && !skip) {
+  if constexpr ((HSPMV_DIAG & 256) != 0) {  // ablation: no y stores (kept live)
+    if (valid && !skip && acc == T(12345.678)) y[row] = acc;
+  } else if (valid && !skip) {
     if (y_nt)  // HBM-resident: streaming stores (bw_probe3/4: y writes cost ~20 % of time)
       __builtin_nontemporal_store(acc, y + row);
     else
@@ -591,6 +607,14 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
   const int wid = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t blk = xcd_chunk_remap(blockIdx.x, gridDim.x, xcd_chunk);
+#if (HSPMV_DIAG & 512)
+  unsigned long long *bt = blk < kTraceWaves ? g_trace + blk * kTraceSlots : nullptr;
+  if (bt && threadIdx.x == 0) {
+    bt[0] = diag_realtime();
+    bt[6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    bt[7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+  }
+#endif
   // XD: the W packed tasks of the block share one staged dictionary
   if constexpr (XD) stage_xdict<T, W * 64>(reinterpret_cast<T *>(xdyn), x, xd, blk, threadIdx.x);
   const int64_t t = blk * W + wid;
@@ -636,6 +660,9 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     beg = nbeg;
     end = nend;
   }
+#if (HSPMV_DIAG & 512)
+  if (bt && lane == 0 && wid < 4) bt[1 + wid] = diag_realtime();
+#endif
 }
 
 // ------------------------------------------------------------------ launchers

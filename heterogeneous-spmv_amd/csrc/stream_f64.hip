@@ -9,9 +9,9 @@ hipError_t launch_rows_f64(const DevCSR &A, const DevPlan &dp, const LaunchPlan 
 }
 }  // namespace hspmv
 
-#if (HSPMV_DIAG & 8)
+#if (HSPMV_DIAG & (8 | 512))
 // Diagnostic builds only: copies the STREAM fp64 kernel's per-wave phase
-// stamps (kTraceWaves x kTraceSlots u64) to host memory `dst`.
+// stamps (8) or the CSR3 kernel's per-workgroup timeline (512) (kTraceWaves x kTraceSlots u64) to host memory `dst`.
 extern "C" int hspmv_diag_trace(void *dst, size_t bytes) {
   const size_t n = sizeof(unsigned long long) * hspmv::dev::kTraceWaves * hspmv::dev::kTraceSlots;
   if (bytes < n) return -1;

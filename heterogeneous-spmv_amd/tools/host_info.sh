@@ -15,6 +15,11 @@ mkdir -p "$(dirname "$O")"
   timeout 60 rocm-smi --showproductname --showbus --showmeminfo vram --showclocks --showfwinfo 2>&1 | grep -v '^$'
   echo "== amd-smi static"; timeout 60 amd-smi static 2>&1 | head -200
   echo "== amd-smi partition"; timeout 60 amd-smi partition 2>&1 | head -60
+  # amdgpu module parameters (mtype_local etc. set the L2 caching mode of
+  # local VRAM) and the kernel command line, where readable
+  echo "== amdgpu module parameters"
+  for f in /sys/module/amdgpu/parameters/*; do [ -r "$f" ] && printf '%s=%s\n' "$(basename $f)" "$(cat $f 2>/dev/null)"; done
+  echo "== kernel cmdline"; cat /proc/cmdline 2>/dev/null
   echo "== rocminfo (agent 2)"; timeout 60 rocminfo 2>&1 | grep -E 'Marketing|Compute Unit|Max Clock|Size:|Segment|L2|Cacheline' | head -40
 } > "$O" 2>&1
 echo "host info -> $O"

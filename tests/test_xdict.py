@@ -34,13 +34,14 @@ def _long_rows():
 
 def block_rows(A, maps, kernel, fill=True):
     """Workgroup row ranges the planner uses (STREAM: 256 rows; CSR3: four
-    tasks, 64-row aligned groups by default, or with HSPMV_TASK_FILL=0
-    whole super-rows packed into <= 64-row tasks; both cut at the budget)."""
+    tasks, 64-row aligned groups by default, or with the packed plan whole
+    super-rows packed into <= 64-row tasks; both cut at the budget, and the
+    workgroups with the largest dictionaries cut in two)."""
     if maps is None or kernel == "stream":
         return np.append(np.arange(0, A.m, 256), A.m)
     if fill:
         starts = cap_tasks(A, list(range(0, A.m, 64)) + [A.m])
-        return np.array(starts[::4] + ([A.m] if (len(starts) - 1) % 4 else []))
+        return cut_blocks(A, starts)
     starts, start = [], 0
     inner = maps.inner
     for sr in range(len(inner) - 1):
@@ -57,7 +58,48 @@ def block_rows(A, maps, kernel, fill=True):
         starts.append(start)
     starts.append(A.m)
     starts = cap_tasks(A, starts)
-    return np.array(starts[::4] + ([A.m] if (len(starts) - 1) % 4 else []))
+    return cut_blocks(A, starts)
+
+
+def dict_entries(A, r0, r1, long_t=4096, gap=8):
+    """x entries a workgroup over rows [r0, r1) stages: its distinct columns
+    as runs, gaps <= gap bridged (doubled until <= 63 runs), split rows out
+    (hspmv_api.cpp plan_xdict)."""
+    lens = np.diff(A.row_ptr)
+    c = np.unique(np.concatenate([A.col_idx[A.row_ptr[r]:A.row_ptr[r + 1]] for r in range(r0, r1)
+                                  if lens[r] <= long_t] or [np.zeros(0, np.int32)]))
+    if len(c) == 0:
+        return 0
+    while True:
+        brk = np.flatnonzero(np.diff(c) > gap)
+        if len(brk) + 1 <= 63:
+            break
+        gap *= 2
+    starts = np.concatenate([[c[0]], c[brk + 1]])
+    ends = np.concatenate([c[brk], [c[-1]]])
+    return int(np.sum(ends - starts + 1))
+
+
+def xd_target(dtype):
+    """Largest dictionary of a 4-task block sized for 6 workgroups per CU
+    (hspmv_api.cpp xd_target_entries: 160 KiB / 6 in 1 KiB granules, minus
+    the product staging of U = 4 fp64 / 16 fp32)."""
+    sv = np.dtype(dtype).itemsize
+    staging = 4 * 64 * (4 if sv == 8 else 16) * sv + 16
+    return (160 * 1024 // 6 // 1024 * 1024 - staging) // sv
+
+
+def cut_blocks(A, starts):
+    """Four tasks per workgroup; a workgroup whose dictionary exceeds
+    xd_target is cut into two of two tasks each (split_xd_blocks)."""
+    target = xd_target(A.val.dtype)
+    out = []
+    for i in range(0, len(starts) - 1, 4):
+        ts = starts[i:i + 5]
+        out.append(ts[0])
+        if len(ts) - 1 > 2 and dict_entries(A, ts[0], ts[-1]) > target:
+            out.append(ts[2])
+    return np.array(out + [A.m])
 
 
 def cap_tasks(A, starts, budget=2048, long_t=4096):
