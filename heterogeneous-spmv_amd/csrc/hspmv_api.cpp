@@ -782,7 +782,10 @@ int64_t xd_target_entries(int dtype, const Tuning &t) {
 
 // Cuts the 4-task blocks of `tasks` whose dictionary exceeds `target`
 // entries into two 2-task blocks padded with empty tasks.  Returns the
-// number of blocks cut.
+// number of blocks cut.  (Cutting the launch's last blocks as well, so its
+// drain runs on workgroups of half the life, measured slower: C3 108.0 ->
+// 110.7 / 112.2 / 115.8 us for the last 768 / 1536 / 3072 blocks, fp32 62.1
+// -> 64.0 / 66.6 / 70.9; profiles/r03/ab_c3_tail_cuts_negative.jsonl.)
 int64_t split_xd_blocks(std::vector<int32_t> &tasks, const std::vector<int32_t> &total,
                         int64_t target) {
   const int64_t nt = (int64_t)tasks.size() - 1, W = 4;
