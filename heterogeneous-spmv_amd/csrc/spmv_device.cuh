@@ -13,7 +13,13 @@ namespace dev {
 // Ablation builds only (make diag): 1 = skip the ordered row sums, 2 = skip
 // the x gather (x[col] := 1), 3 = both; 16 = skip the x-dictionary staging
 // (and its barrier), 32 = the barrier without the staging loads, 256 = no y
-// stores (the sums kept live).  Results are wrong in those builds.
+// stores (the sums kept live), 1024 = 1-byte dictionary positions (half the
+// index bytes; the bound on any position compression: C3 107.3 -> 102.7 us,
+// fp32 62.1 -> 51.2, profiles/r03/ab_c3_1byte_positions_ablation.jsonl --
+// run-coded positions (a run-start mask per 64 nonzeros + 2 bytes per run,
+// 0.86 B/nnz on C3) measured 108.7 -> 114.2 us, fp32 62.2 -> 99.4: the
+// decode's dependent loads cost more than the bytes).  Results are wrong in
+// those builds.
 #ifndef HSPMV_DIAG
 #define HSPMV_DIAG 0
 #endif
@@ -304,7 +310,9 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         for (int u = 0; u < U; ++u) {
           // clamp instead of branching: every load issues back to back
           const uint32_t j = (uint32_t)(c0 + min(u * kWave + lane, last));
-          if constexpr (XD) {
+          if constexpr (XD && (HSPMV_DIAG & 1024) != 0) {
+            col[u] = (int32_t)ld_off<NT, uint8_t>(cb, j);  // ablation: 1-byte positions (wrong x)
+          } else if constexpr (XD) {
             col[u] = (int32_t)ld_off<NT, uint16_t>(cb, j * 2u);  // position in the block's xs
           } else if constexpr (C16 == 2) {
             // group-base offsets: col = the 64-row group's smallest column
