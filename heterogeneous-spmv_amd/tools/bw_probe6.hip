@@ -18,6 +18,8 @@
 //               launches timed together: reads and writes never overlap)
 //   <v> G=k   : each workgroup takes k consecutive 256-row segments in turn
 //               (a wave's y store overlaps its next segment's loads)
+//   y.reg G=k : each wave keeps its k segments' sums in registers and stores
+//               them after the last one (no store between a wave's loads)
 //   y.defer   : persistent grid (256 CUs x 8 blocks), each block keeps its
 //               rows' y in LDS and stores them all after its last segment
 // Reported: ms (min of 10) and effective GB/s over the stream + y bytes.
@@ -40,7 +42,7 @@
     }                                                                               \
   } while (0)
 
-enum { Y_NONE = 0, Y_WAVE = 1, Y_L2 = 2, Y_BLOCK = 3, Y_NT = 4, Y_X4 = 5, Y_BX4 = 6, Y_LANE0 = 7 };
+enum { Y_NONE = 0, Y_WAVE = 1, Y_L2 = 2, Y_BLOCK = 3, Y_NT = 4, Y_X4 = 5, Y_BX4 = 6, Y_LANE0 = 7, Y_REG = 8 };
 constexpr int U = 4;
 
 // one wave's 64 rows: returns this lane's row sum
@@ -76,6 +78,7 @@ __global__ __launch_bounds__(256) void probe(const uint16_t *__restrict__ pos,
   __shared__ double lds[4 * 64 * UU];
   __shared__ double ys[256];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double keep[G];
   for (int gi = 0; gi < G; ++gi) {
   const long w = ((long)blockIdx.x * G + gi) * 4 + wid;
   const long r = w * 64 + lane;
@@ -108,6 +111,8 @@ __global__ __launch_bounds__(256) void probe(const uint16_t *__restrict__ pos,
       *reinterpret_cast<double2 *>(y + rb + 4 * lane) = make_double2(t.x, t.y);
       *reinterpret_cast<double2 *>(y + rb + 4 * lane + 2) = make_double2(t.z, t.w);
     }
+  } else if constexpr (MODE == Y_REG) {
+    keep[gi] = s;  // stored after the last segment
   } else if constexpr (MODE == Y_LANE0) {
     if (lane == 0 && r < m) y[r] = s;  // 8 B per wave: one store, one lane
   } else if constexpr (MODE == Y_BLOCK) {
@@ -116,6 +121,13 @@ __global__ __launch_bounds__(256) void probe(const uint16_t *__restrict__ pos,
     const long rb = (long)blockIdx.x * 256;
     if (rb + threadIdx.x < m) y[rb + threadIdx.x] = ys[threadIdx.x];
   }
+  }
+  if constexpr (MODE == Y_REG) {
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      const long r = (((long)blockIdx.x * G + gi) * 4 + wid) * 64 + lane;
+      if (r < m) y[r] = keep[gi];
+    }
   }
 }
 
@@ -326,7 +338,19 @@ int main(int argc, char **argv) {
     const float ms = time_ms([&] { hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, 0, pos, val, y, m, per, out); }, 10);
     report(name, ms, bytes);
   };
-  for (int rep = 0; rep < 2; ++rep) {
+  const bool reg_only = argc > 3 && atoi(argv[3]) == 1;
+  for (int rep = 0; rep < 2 && reg_only; ++rep) {
+    run(probe<Y_NONE>, "base", sb);
+    run(probe<Y_WAVE>, "y.wave", sb + yb);
+    run(probe<Y_NONE, 2>, "base G=2", sb, 2);
+    run(probe<Y_REG, 2>, "y.reg G=2", sb + yb, 2);
+    run(probe<Y_WAVE, 2>, "y.wave G=2", sb + yb, 2);
+    run(probe<Y_NONE, 4>, "base G=4", sb, 4);
+    run(probe<Y_REG, 4>, "y.reg G=4", sb + yb, 4);
+    run(probe<Y_NONE, 8>, "base G=8", sb, 8);
+    run(probe<Y_REG, 8>, "y.reg G=8", sb + yb, 8);
+  }
+  for (int rep = 0; rep < 2 && !reg_only; ++rep) {
     run(probe<Y_NONE>, "base", sb);
     run(probe<Y_WAVE>, "y.wave", sb + yb);
     run(probe<Y_L2>, "y.l2", sb + yb);
