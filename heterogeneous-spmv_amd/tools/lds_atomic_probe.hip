@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define CHECK(x)                                                                     \
   do {                                                                               \
@@ -30,7 +31,7 @@ __device__ __forceinline__ uint32_t hash32(uint32_t v) {
 
 // Every thread adds ITER values into random slots of an S-slot LDS array
 // (S dynamic), then the block writes its slots out (so nothing is elided).
-template <typename T, int ITER>
+template <typename T, int ITER, bool SEQ = false>
 __global__ __launch_bounds__(1024) void probe(int32_t slots, uint32_t seed, T *out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T *acc = reinterpret_cast<T *>(smem);
@@ -40,26 +41,30 @@ __global__ __launch_bounds__(1024) void probe(int32_t slots, uint32_t seed, T *o
 #pragma unroll 16
   for (int it = 0; it < ITER; ++it) {
     h = h * 1664525u + 1013904223u;  // LCG: 2 VALU ops
-    const int s = (int)__umulhi(h, (uint32_t)slots);
+    // SEQ: lane-consecutive slots (no bank conflicts), a random base per
+    // wave instruction -- the ceiling a conflict-free arrangement could reach
+    const int s = SEQ ? (int)((__builtin_amdgcn_readfirstlane(__umulhi(h, (uint32_t)slots)) +
+                               (threadIdx.x & 63)) % (uint32_t)slots)
+                      : (int)__umulhi(h, (uint32_t)slots);
     atomicAdd(&acc[s], (T)(h & 7u));
   }
   __syncthreads();
   for (int i = threadIdx.x; i < slots; i += blockDim.x) out[(size_t)blockIdx.x * slots + i] = acc[i];
 }
 
-template <typename T>
+template <typename T, bool SEQ = false>
 int run(const char *name, int slots, int blocks, hipEvent_t a, hipEvent_t b) {
   constexpr int ITER = 256;
   T *out = nullptr;
   CHECK(hipMalloc(&out, sizeof(T) * (size_t)slots * blocks));
   const size_t lds = sizeof(T) * (size_t)slots;
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((probe<T, ITER>), dim3(blocks), dim3(1024), lds, 0, slots, 1u, out);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((probe<T, ITER, SEQ>), dim3(blocks), dim3(1024), lds, 0, slots, 1u, out);
   CHECK(hipGetLastError());
   CHECK(hipDeviceSynchronize());
   float best = 1e30f;
   for (int r = 0; r < 5; ++r) {
     CHECK(hipEventRecord(a, 0));
-    hipLaunchKernelGGL((probe<T, ITER>), dim3(blocks), dim3(1024), lds, 0, slots, (uint32_t)r + 7u, out);
+    hipLaunchKernelGGL((probe<T, ITER, SEQ>), dim3(blocks), dim3(1024), lds, 0, slots, (uint32_t)r + 7u, out);
     CHECK(hipEventRecord(b, 0));
     CHECK(hipEventSynchronize(b));
     float ms = 0.f;
@@ -81,6 +86,13 @@ int main() {
   CHECK(hipEventCreate(&b));
   // csort today: 256 workgroups of ~15.6 K fp64 slots (one per CU); the
   // two-per-CU shapes: 512 workgroups of ~7.8 K fp64 or ~15.6 K fp32 slots
+  if (getenv("LDS_PROBE_SEQ")) {  // conflict-free ceilings vs random, csort's shape
+    const int s = 16000, g = 256;
+    if (run<double>("f64", s, g, a, b) || run<double, true>("f64 seq", s, g, a, b)) return 1;
+    if (run<unsigned long long>("u64", s, g, a, b) || run<unsigned long long, true>("u64 seq", s, g, a, b)) return 1;
+    if (run<float>("f32", s, g, a, b) || run<float, true>("f32 seq", s, g, a, b)) return 1;
+    return 0;
+  }
   const int cases[][2] = {{16000, 256}, {7800, 512}, {16000, 512}, {4000, 512}};
   for (auto &c : cases) {
     const int s = c[0], g = c[1];
