@@ -34,6 +34,14 @@
 
 #include "hspmv_internal.h"
 
+// Ablation builds only (wrong results by design; tools: the csort-abl
+// libraries of the Makefile): 1 = the slot adds as ds_add_u64 of the bit
+// pattern, 2 = no slot adds (products summed in a register), 3 = a plain LDS
+// read of the slot instead of the add.
+#ifndef HSPMV_CSORT_ABL
+#define HSPMV_CSORT_ABL 0
+#endif
+
 namespace hspmv {
 namespace {
 
@@ -180,6 +188,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
   uint32_t ix[U];
   T vv[U];
+  S sink = S(0);  // ablation builds only
   // PF: the next chunk's entries are loaded while this chunk's gathers are
   // in flight (software pipelining across the wave's chunks)
   if constexpr (PF)
@@ -213,7 +222,19 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
           pr = (double)vvc[u] * (double)xv[u];  // exact
         else
           pr = (S)(vvc[u] * xv[u]);  // omp_spmv's rounded product
+#if HSPMV_CSORT_ABL == 1
+        if constexpr (sizeof(S) == 8)
+          atomicAdd(reinterpret_cast<unsigned long long *>(&acc[ixc[u] >> 16]),
+                    (unsigned long long)__builtin_bit_cast(long long, pr));
+        else
+          atomicAdd(&acc[ixc[u] >> 16], pr);
+#elif HSPMV_CSORT_ABL == 2
+        sink += pr + (S)(ixc[u] >> 16);
+#elif HSPMV_CSORT_ABL == 3
+        sink += pr * acc[ixc[u] >> 16];
+#else
         atomicAdd(&acc[ixc[u] >> 16], pr);
+#endif
       }
     } else {
       // Segmented chunk: the host found rows whose entries crowd one
@@ -245,6 +266,9 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
       }
     }
   }
+#if HSPMV_CSORT_ABL == 2 || HSPMV_CSORT_ABL == 3
+  if (sink != S(0)) atomicAdd(&acc[nr + nv], sink);  // the dummy slot: keeps the products live
+#endif
   __syncthreads();
   if (trace && threadIdx.x == 0) trace[3 * b + 1] = __builtin_amdgcn_s_memrealtime();
   if (direct) {  // one column part, no long rows: y straight from the slots
