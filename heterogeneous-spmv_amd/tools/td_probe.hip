@@ -19,6 +19,10 @@
 //              1.5 entries per 32-byte sector, 8 per lane per chunk
 //   glds16+lg: glds16 into a 16 KiB per-workgroup window, then the same
 //              gathers as `gather` served from LDS (the staged design)
+//   win      : the same entries as `gather`, but per 64-entry instruction the
+//              x span it covers is loaded coalesced (16 B per lane, lanes past
+//              the span masked) into a 2 KiB per-wave LDS window and the lanes
+//              read their entries from there (fewer, wider L1 accesses)
 // Reported: ms (min of 10), GB/s of the 1 GiB read (x halves x 128
 // workgroups), and for the gathers ns per workgroup entry.
 //
@@ -45,7 +49,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void glb_void;
 
-enum { LD4 = 0, LD16 = 1, GLDS4 = 2, GLDS16 = 3, GATHER = 4, GLDS_GATHER = 5 };
+enum { LD4 = 0, LD16 = 1, GLDS4 = 2, GLDS16 = 3, GATHER = 4, GLDS_GATHER = 5, WIN_GATHER = 6 };
 
 // entries of a workgroup: e = 0 .. kEnt-1 at column (e * 16) / 3 of its half
 constexpr long kEnt = kHalf * 3 / 16;
@@ -99,6 +103,37 @@ __global__ __launch_bounds__(kThreads) void probe(const float *__restrict__ x, f
       for (int u = 0; u < 8; ++u) {
         const long e = std::min(c * 512 + u * 64 + lane, kEnt - 1);
         v[u] = xh[(e * 16) / 3];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+  } else if constexpr (MODE == WIN_GATHER) {
+    float *win = smem + wid * 512;  // 2 KiB per wave
+    const f32x4 *p4 = reinterpret_cast<const f32x4 *>(xh);
+    for (long c = wid; c * 512 < kEnt; c += kWaves) {
+      f32x4 w0[8], w1[8];
+      int32_t base[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const long e0 = std::min(c * 512 + u * 64, kEnt - 1), e1 = std::min(e0 + 63, kEnt - 1);
+        base[u] = (int32_t)(((e0 * 16) / 3) & ~3L);
+        const int32_t nq = (int32_t)((((e1 * 16) / 3) - base[u]) / 4 + 1);  // <= 128
+        w0[u] = lane < nq ? p4[base[u] / 4 + lane] : f32x4{0, 0, 0, 0};
+        w1[u] = lane + 64 < nq ? p4[base[u] / 4 + 64 + lane] : f32x4{0, 0, 0, 0};
+      }
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        *reinterpret_cast<f32x4 *>(win + lane * 4) = w0[u];
+        *reinterpret_cast<f32x4 *>(win + 256 + lane * 4) = w1[u];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const long e = std::min(c * 512 + u * 64 + lane, kEnt - 1);
+        v[u] = win[(int32_t)((e * 16) / 3) - base[u]];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc += v[u];
@@ -158,18 +193,20 @@ int main() {
   CK(hipFuncSetAttribute((const void *)probe<GLDS16>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   CK(hipFuncSetAttribute((const void *)probe<GATHER>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   CK(hipFuncSetAttribute((const void *)probe<GLDS_GATHER>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  CK(hipFuncSetAttribute((const void *)probe<WIN_GATHER>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   const double bytes = (double)kBlocks * kHalf * 4;
-  const char *names[] = {"ld4", "ld16", "glds4", "glds16", "gather", "glds16+lg"};
-  float ms[6];
+  const char *names[] = {"ld4", "ld16", "glds4", "glds16", "gather", "glds16+lg", "win"};
+  float ms[7];
   ms[0] = run<LD4>(x, out, st, lds);
   ms[1] = run<LD16>(x, out, st, lds);
   ms[2] = run<GLDS4>(x, out, st, lds);
   ms[3] = run<GLDS16>(x, out, st, lds);
   ms[4] = run<GATHER>(x, out, st, lds);
   ms[5] = run<GLDS_GATHER>(x, out, st, lds);
+  ms[6] = run<WIN_GATHER>(x, out, st, lds);
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
-  for (int i = 0; i < 6; ++i)
+  for (int i = 0; i < 7; ++i)
     printf("{\"probe\": \"td\", \"mode\": \"%s\", \"ms\": %.4f, \"x_GBps\": %.1f, \"ns_per_wg_entry\": %.4f}\n",
            names[i], ms[i], bytes / (ms[i] * 1e-3) / 1e9, ms[i] * 1e6 / kEnt);
   return 0;
