@@ -12,7 +12,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <array>
 #include <cstddef>
 #include <cmath>
 #include <cstdlib>
@@ -185,7 +184,6 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_CSORT_BPC", &t->csort_blocks_per_cu);
   geti("HSPMV_CSORT_SLOT32", &t->csort_slot32);
   geti("HSPMV_CSORT_WIDE", &t->csort_wide);
-  geti("HSPMV_CSORT_COMPACT", &t->csort_compact);
   geti("HSPMV_CSORT_LDS", &t->csort_lds_cap);
   geti("HSPMV_CSORT_SEG", &t->csort_seg);
   geti("HSPMV_CSORT_SEG_EXTRA", &t->csort_seg_extra);
@@ -1020,7 +1018,6 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
 // Tuning.csort_parts = 1/2/4 sets the column parts, csort_u = 4/8/16 the
 // chunk.  The row blocks are capped by the device's LDS per workgroup.
 constexpr int32_t kCsortSlice = 2048;
-constexpr bool kCsortCompact = false;  // 7-byte fp32 entries by default (A/B: csort_compact)
 // a chunk whose instructions would serialise more than this many same-slot
 // lanes in all is stored slot-sorted (segmented)
 constexpr int64_t kCsortSegExtra = 128;
@@ -1179,7 +1176,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   }
   // per workgroup: sorted entries, chunk count (pass 1)
   std::vector<std::vector<CsEnt>> ents((size_t)G);
-  std::vector<int64_t> nchunks((size_t)G, 0), ncomp((size_t)G, 0);
+  std::vector<int64_t> nchunks((size_t)G, 0);
   std::vector<int32_t> nslots((size_t)G, 0);
   const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, G / 4));
   std::atomic<bool> too_big{false};
@@ -1197,48 +1194,6 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     }
     return cnt_;
   };
-  // Compact 7-byte fp32 entries (kernel: csort.hip load_entries WIDE == 2):
-  // instructions of <= 64 entries whose columns span <= 511 (9-bit offsets
-  // from a per-instruction base), U instructions per chunk, slots < 2^15.
-  // C5: 8 -> 7 bytes per nonzero of the HBM entry stream.  Segmented
-  // chunks keep the 8-byte layout (their instructions mix rows' columns).
-  bool compact = dtype == HSPMV_F32 && !slot32 && U % 4 == 0 && wide &&
-                 (tn.csort_compact >= 0 ? tn.csort_compact == 1 : kCsortCompact);
-  auto walk_compact = [&](const std::vector<CsEnt> &E, auto &&emit) {
-    // emit(ci, ins) with ins[u] = {begin, end, base} for u < U
-    int64_t i = 0, cnt_ = 0;
-    const int64_t ne = (int64_t)E.size();
-    std::array<std::array<int64_t, 3>, 16> ins{};
-    while (i < ne) {
-      for (int u = 0; u < U; ++u) {
-        const int64_t b0 = i;
-        const uint32_t c0 = i < ne ? E[(size_t)i].col : 0u;
-        while (i < ne && i - b0 < 64 && E[(size_t)i].col - c0 <= 511u) ++i;
-        ins[(size_t)u] = {b0, i, (int64_t)c0};
-      }
-      emit(cnt_, ins);
-      ++cnt_;
-    }
-    return cnt_;
-  };
-  // the segmented-chunk rule on a compact chunk: serialised same-slot lanes
-  auto seg_extra = [&](const std::vector<CsEnt> &E, int64_t i, int64_t j) {
-    uint32_t sl64[64];
-    int64_t extra = 0;
-    for (int64_t g = i; g < j; g += 64) {
-      const int64_t e = std::min(j, g + 64);
-      for (int64_t t = g; t < e; ++t) sl64[t - g] = E[(size_t)t].slot;
-      std::sort(sl64, sl64 + (e - g));
-      int run = 1, mx = 1;
-      for (int64_t t = 1; t < e - g; ++t) {
-        run = sl64[t] == sl64[t - 1] ? run + 1 : 1;
-        mx = std::max(mx, run);
-      }
-      extra += mx - 1;
-    }
-    return extra;
-  };
-  std::atomic<bool> compact_ok{compact};
   {
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t)
@@ -1261,22 +1216,11 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
           nslots[(size_t)b] = nr + (int32_t)sl.size() + 1;  // + the dummy slot
           if (nslots[(size_t)b] > 65536 || ((int64_t)nslots[(size_t)b] + 1) * slot_bytes > lds_max) too_big = true;
           nchunks[(size_t)b] = chunk_walk(E, [](int64_t, uint32_t, int64_t, int64_t) {});
-          if (compact_ok) {
-            if (nslots[(size_t)b] > 32768) compact_ok = false;
-            const int64_t lim = tn.csort_seg_extra > 0 ? tn.csort_seg_extra : kCsortSegExtra;
-            ncomp[(size_t)b] = walk_compact(E, [&](int64_t, const auto &ins) {
-              if (tn.csort_seg == 2 ||
-                  (tn.csort_seg != 0 && seg_extra(E, ins[0][0], ins[(size_t)U - 1][1]) > lim))
-                compact_ok = false;
-            });
-          }
         }
       });
     for (auto &x : th) x.join();
   }
   if (too_big) return HSPMV_OK;
-  compact = compact && compact_ok;
-  if (compact) nchunks.swap(ncomp);
   std::vector<int32_t> blk_c((size_t)G + 1, 0), blk_v((size_t)G + 1, 0), vslice;
   int64_t tot_chunks = 0;
   int32_t max_slots_used = 1;
@@ -1292,14 +1236,11 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   if (tot_chunks * C >= (int64_t)1 << 40 || tot_chunks >= INT32_MAX) return HSPMV_OK;
   const int64_t tot = tot_chunks * C;
   // pass 2: the device arrays
-  std::vector<int32_t> cbase((size_t)std::max<int64_t>(tot_chunks * (compact ? U : 1), 1), 0);
+  std::vector<int32_t> cbase((size_t)std::max<int64_t>(tot_chunks, 1), 0);
   std::vector<uint32_t> idx;
   std::vector<uint64_t> rec;
-  std::vector<unsigned char> rec7;
   std::vector<double> val64;
-  if (compact)
-    rec7.assign((size_t)tot * 7, 0);
-  else if (dtype == HSPMV_F32)
+  if (dtype == HSPMV_F32)
     rec.assign((size_t)tot, 0);
   else {
     idx.assign((size_t)tot, 0);
@@ -1321,34 +1262,6 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
             const int64_t u = q / 64, lane = q % 64;
             return (u / per) * (64 * per) + lane * per + (u % per);
           };
-          if (compact) {
-            walk_compact(E, [&](int64_t ci, const auto &ins) {
-              const int64_t ch = cfirst + ci;
-              unsigned char *cp = rec7.data() + (size_t)ch * (size_t)C * 7;
-              for (int u = 0; u < U; ++u) {
-                const int64_t b0 = ins[(size_t)u][0], b1 = ins[(size_t)u][1];
-                const uint32_t base = (uint32_t)ins[(size_t)u][2];
-                cbase[(size_t)(ch * U + u)] = (int32_t)base;
-                unsigned char *gp = cp + (size_t)(u / 4) * 1792;
-                const int k = u % 4;
-                for (int64_t q = 0; q < 64; ++q) {
-                  uint32_t slot = dummy, off = 0, vb = 0;
-                  if (b0 + q < b1) {
-                    const CsEnt &e = E[(size_t)(b0 + q)];
-                    slot = e.slot;
-                    off = e.col - base;
-                    memcpy(&vb, (const char *)val + 4 * (size_t)e.k, 4);
-                  }
-                  const uint16_t w = (uint16_t)(slot | ((off >> 8) << 15));
-                  memcpy(gp + q * 16 + k * 4, &vb, 4);
-                  memcpy(gp + 1024 + q * 8 + k * 2, &w, 2);
-                  gp[1536 + q * 4 + k] = (unsigned char)(off & 0xffu);
-                }
-              }
-            });
-            std::vector<CsEnt>().swap(E);
-            continue;
-          }
           std::vector<CsEnt> tmp;
           uint32_t sl64[64];
           chunk_walk(E, [&](int64_t ci, uint32_t c0, int64_t i, int64_t j) {
@@ -1446,11 +1359,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   if ((rc = up(&s.d_cs_blk_c, blk_c)) || (rc = up(&s.d_cs_blk_r, wg_rows)) ||
       (rc = up(&s.d_cs_blk_v, blk_v)) || (rc = up(&s.d_cs_vslice, vslice)) || (rc = up(&s.d_cs_cbase, cbase)))
     return rc;
-  if (compact) {
-    unsigned char *d = nullptr;
-    if ((rc = up(&d, rec7))) return rc;
-    s.d_cs_ent = d;
-  } else if (dtype == HSPMV_F32) {
+  if (dtype == HSPMV_F32) {
     uint64_t *d = nullptr;
     if ((rc = up(&d, rec))) return rc;
     s.d_cs_ent = d;
@@ -1487,7 +1396,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.prefetch = wide && dtype == HSPMV_F32;  // see `wide` above
   if (tn.csort_pf >= 0) c.prefetch = tn.csort_pf != 0;
   c.slot32 = slot32;
-  c.wide = compact ? 2 : (wide ? 1 : 0);
+  c.wide = wide;
   c.m = m;
   c.lds_bytes = (int32_t)(slot_bytes * max_slots_used);
   c.blk_c = s.d_cs_blk_c;

@@ -65,7 +65,6 @@ struct Tuning {
   int csort_blocks_per_cu = 0;           // row blocks per CU and part (0: 1)
   int csort_slot32 = -1;                 // fp32 LDS row slots (fp32 data)
   int csort_wide = -1;                   // 16-byte entry loads (interleaved layout)
-  int csort_compact = -1;                // 7-byte fp32 entries (per-instruction bases)
   int csort_lds_cap = 0;                 // LDS bytes per workgroup for the row slots (0: all)
   int csort_seg = -1;                    // segmented chunks: 0 never, 2 always (-1: by conflicts)
   int csort_seg_extra = 0;               // serialised same-slot lanes that flag a chunk (0: default)
@@ -98,7 +97,7 @@ struct DevCsort {
   bool nontemporal = true;
   bool prefetch = false;  // next chunk's entries loaded during this chunk's gathers
   bool slot32 = false;    // fp32 LDS row slots and partials (fp32 data; A/B)
-  int wide = 0;           // 1: 16-byte entry loads (host-interleaved layout); 2: compact 7-byte fp32 entries
+  bool wide = false;      // 16-byte entry loads (host-interleaved layout)
   int64_t m = 0;
   int32_t lds_bytes = 0;
   const int32_t *blk_c = nullptr, *blk_r = nullptr, *blk_v = nullptr, *vslice = nullptr;
