@@ -34,11 +34,11 @@
 
 #include "hspmv_internal.h"
 
-// Ablation builds only (wrong results by design; tools: the csort-abl
-// libraries of the Makefile): 1 = the slot adds as ds_add_u64 of the bit
-// pattern, 2 = no slot adds (products summed in a register), 3 = a plain LDS
-// read of the slot instead of the add, 4 = every gather of a chunk within
-// the chunk's first x sector (the x sweep removed, the entry stream kept).
+// Ablation builds only (wrong results by design; the csort-abl libraries of
+// the Makefile): 1 = the slot adds as ds_add_u64 of the bit pattern, 2 = no
+// slot adds (products summed in a register), 3 = a plain LDS read of the
+// slot instead of the add, 4 = every gather of a chunk within the chunk's
+// first x sector (the x sweep removed, the entry stream kept).
 #ifndef HSPMV_CSORT_ABL
 #define HSPMV_CSORT_ABL 0
 #endif
@@ -109,37 +109,11 @@ __device__ __forceinline__ S seg_scan(S v, uint32_t k) {
 // interleaved on the host (build_csort) so that one load brings the lane
 // two (fp32 records, fp64 values) or four (fp64 indices) of its entries;
 // the entry -> (u, lane) mapping, and so every gather, is unchanged.
-// WIDE == 2 (fp32, U % 4 == 0): the 7-byte compact layout (kCsortCompact,
-// build_csort): per group of four instructions 1792 bytes -- the 64 lanes'
-// four values (16 B each), their four 16-bit words (8 B each: slot in bits
-// 0-14, bit 15 = bit 8 of the column offset) and their four low offset bytes
-// (4 B each); the offset is from the INSTRUCTION's base column (cbase[c*U+u]).
-template <typename T, int U, bool NT, int WIDE>
+template <typename T, int U, bool NT, bool WIDE>
 __device__ __forceinline__ void load_entries(const void *__restrict__ ent, const T *__restrict__ val,
                                              int32_t c, int lane, uint32_t (&ix)[U], T (&vv)[U]) {
   const int64_t k0 = (int64_t)c * (kWave * U);
-  if constexpr (WIDE == 2) {
-    static_assert(sizeof(T) == 4 && U % 4 == 0, "compact entries: fp32, U multiple of 4");
-    const unsigned char *g0 = reinterpret_cast<const unsigned char *>(ent) + (int64_t)c * (U / 4) * 1792;
-#pragma unroll
-    for (int g = 0; g < U / 4; ++g) {
-      const unsigned char *gp = g0 + g * 1792;
-      const u32x4 v = ld<NT>(reinterpret_cast<const u32x4 *>(gp) + lane);
-      const u32x2 lo = ld<NT>(reinterpret_cast<const u32x2 *>(gp + 1024) + lane);
-      const uint32_t hi = ld<NT>(reinterpret_cast<const uint32_t *>(gp + 1536) + lane);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t w = ((k < 2 ? lo.x : lo.y) >> (16 * (k & 1))) & 0xffffu;
-        ix[4 * g + k] = ((w & 0x7fffu) << 16) | ((w >> 15) << 8) | ((hi >> (8 * k)) & 0xffu);
-      }
-      vv[4 * g] = __uint_as_float(v.x);
-      vv[4 * g + 1] = __uint_as_float(v.y);
-      vv[4 * g + 2] = __uint_as_float(v.z);
-      vv[4 * g + 3] = __uint_as_float(v.w);
-    }
-    return;
-  }
-  if constexpr (WIDE == 1) {
+  if constexpr (WIDE) {
     if constexpr (sizeof(T) == 4) {  // records of entries u*64 + lane, (u+1)*64 + lane side by side
       const u32x4 *p = reinterpret_cast<const u32x4 *>(reinterpret_cast<const u32x2 *>(ent) + k0) + lane;
 #pragma unroll
@@ -188,7 +162,7 @@ __device__ __forceinline__ void load_entries(const void *__restrict__ ent, const
 
 // S: the LDS row-slot / partial-sum type (double; float only for fp32 data,
 // an A/B variant with half the LDS per row).
-template <typename T, typename S, int U, bool NT, bool PF, int WIDE>
+template <typename T, typename S, int U, bool NT, bool PF, bool WIDE>
 __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     int32_t H, int64_t m, int32_t direct, const int32_t *__restrict__ blk_c,
     const int32_t *__restrict__ blk_r, const int32_t *__restrict__ blk_v,
@@ -223,11 +197,8 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   if constexpr (PF)
     if (c0 + wid < c1) load_entries<T, U, NT, WIDE>(ent, val, c0 + wid, lane, ix, vv);
   for (int32_t c = c0 + wid; c < c1; c += NW) {  // wave-uniform
-    // bit 31 of the chunk base: a "segmented" chunk (see below); compact
-    // layout: one base per instruction, the chunk's first carries the flag
-    constexpr int NB = WIDE == 2 ? U : 1;
-    const int32_t *cbc = cbase + (int64_t)wave_uniform(c) * NB;
-    const uint32_t cb = (uint32_t)wave_uniform(cbc[0]);
+    // bit 31 of the chunk base: a "segmented" chunk (see below)
+    const uint32_t cb = (uint32_t)wave_uniform(cbase[wave_uniform(c)]);
     const int32_t base = (int32_t)(cb & 0x7fffffffu);
     const bool seg = (cb >> 31) != 0u;
     if constexpr (!PF) load_entries<T, U, NT, WIDE>(ent, val, c, lane, ix, vv);
@@ -236,10 +207,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
 #if HSPMV_CSORT_ABL == 4
     for (int u = 0; u < U; ++u) xv[u] = x[base + (int32_t)(ix[u] & 0x7u)];  // one x sector per chunk
 #else
-    for (int u = 0; u < U; ++u) {
-      const int32_t bu = WIDE == 2 ? (int32_t)((uint32_t)wave_uniform(cbc[u]) & 0x7fffffffu) : base;
-      xv[u] = x[bu + (int32_t)(ix[u] & 0xffffu)];
-    }
+    for (int u = 0; u < U; ++u) xv[u] = x[base + (int32_t)(ix[u] & 0xffffu)];
 #endif
     uint32_t ixc[U];
     T vvc[U];
@@ -372,7 +340,7 @@ __global__ __launch_bounds__(256) void hspmv_csort_finish(
   if (lane == 0) y[long_row[j]] = (T)s;
 }
 
-template <typename T, typename S, int U, bool NT, bool PF, int WIDE>
+template <typename T, typename S, int U, bool NT, bool PF, bool WIDE>
 void launch_csort_main(const DevCsort &c, const T *x, S *part, S *spart, T *y, hipStream_t st) {
   hipLaunchKernelGGL((hspmv_csort<T, S, U, NT, PF, WIDE>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
                      (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
@@ -385,32 +353,15 @@ hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
   S *part = static_cast<S *>(c.part), *spart = static_cast<S *>(c.spart);
   if constexpr (sizeof(T) == 8 && U % 4 != 0) {
     if (c.wide) return hipErrorInvalidValue;
-    if (c.prefetch) launch_csort_main<T, S, U, NT, true, 0>(c, x, part, spart, y, st);
-    else launch_csort_main<T, S, U, NT, false, 0>(c, x, part, spart, y, st);
-  } else if constexpr (sizeof(T) == 4 && sizeof(S) == 8 && U % 4 == 0) {
-    // fp32 records with fp64 slots: 8-byte, 16-byte or compact 7-byte entries
-    switch (c.wide) {
-      case 0:
-        if (c.prefetch) launch_csort_main<T, S, U, NT, true, 0>(c, x, part, spart, y, st);
-        else launch_csort_main<T, S, U, NT, false, 0>(c, x, part, spart, y, st);
-        break;
-      case 1:
-        if (c.prefetch) launch_csort_main<T, S, U, NT, true, 1>(c, x, part, spart, y, st);
-        else launch_csort_main<T, S, U, NT, false, 1>(c, x, part, spart, y, st);
-        break;
-      default:
-        if (c.prefetch) launch_csort_main<T, S, U, NT, true, 2>(c, x, part, spart, y, st);
-        else launch_csort_main<T, S, U, NT, false, 2>(c, x, part, spart, y, st);
-        break;
-    }
+    if (c.prefetch) launch_csort_main<T, S, U, NT, true, false>(c, x, part, spart, y, st);
+    else launch_csort_main<T, S, U, NT, false, false>(c, x, part, spart, y, st);
   } else {
-    if (c.wide == 2) return hipErrorInvalidValue;
     if (c.prefetch) {
-      if (c.wide) launch_csort_main<T, S, U, NT, true, 1>(c, x, part, spart, y, st);
-      else launch_csort_main<T, S, U, NT, true, 0>(c, x, part, spart, y, st);
+      if (c.wide) launch_csort_main<T, S, U, NT, true, true>(c, x, part, spart, y, st);
+      else launch_csort_main<T, S, U, NT, true, false>(c, x, part, spart, y, st);
     } else {
-      if (c.wide) launch_csort_main<T, S, U, NT, false, 1>(c, x, part, spart, y, st);
-      else launch_csort_main<T, S, U, NT, false, 0>(c, x, part, spart, y, st);
+      if (c.wide) launch_csort_main<T, S, U, NT, false, true>(c, x, part, spart, y, st);
+      else launch_csort_main<T, S, U, NT, false, false>(c, x, part, spart, y, st);
     }
   }
   hipError_t e = hipGetLastError();
