@@ -18,6 +18,8 @@
 //               launches timed together: reads and writes never overlap)
 //   <v> G=k   : each workgroup takes k consecutive 256-row segments in turn
 //               (a wave's y store overlaps its next segment's loads)
+//   y.xchg    : the store as a no-return 64-bit atomic exchange
+//   y.agent   : a relaxed atomic store at agent scope
 //   y.reg G=k : each wave keeps its k segments' sums in registers and stores
 //               them after the last one (no store between a wave's loads)
 //   y.defer   : persistent grid (256 CUs x 8 blocks), each block keeps its
@@ -42,7 +44,7 @@
     }                                                                               \
   } while (0)
 
-enum { Y_NONE = 0, Y_WAVE = 1, Y_L2 = 2, Y_BLOCK = 3, Y_NT = 4, Y_X4 = 5, Y_BX4 = 6, Y_LANE0 = 7, Y_REG = 8 };
+enum { Y_NONE = 0, Y_WAVE = 1, Y_L2 = 2, Y_BLOCK = 3, Y_NT = 4, Y_X4 = 5, Y_BX4 = 6, Y_LANE0 = 7, Y_REG = 8, Y_XCHG = 9, Y_SC = 10 };
 constexpr int U = 4;
 
 // one wave's 64 rows: returns this lane's row sum
@@ -111,6 +113,14 @@ __global__ __launch_bounds__(256) void probe(const uint16_t *__restrict__ pos,
       *reinterpret_cast<double2 *>(y + rb + 4 * lane) = make_double2(t.x, t.y);
       *reinterpret_cast<double2 *>(y + rb + 4 * lane + 2) = make_double2(t.z, t.w);
     }
+  } else if constexpr (MODE == Y_XCHG) {
+    // the y store as a no-return atomic exchange (processed at the L2)
+    if (r < m) (void)__hip_atomic_exchange(reinterpret_cast<unsigned long long *>(y + r),
+                                          (unsigned long long)__builtin_bit_cast(long long, s),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (MODE == Y_SC) {
+    // the y store with device scope (sc1): written through to L2 at once
+    if (r < m) __hip_atomic_store(y + r, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else if constexpr (MODE == Y_REG) {
     keep[gi] = s;  // stored after the last segment
   } else if constexpr (MODE == Y_LANE0) {
@@ -339,6 +349,16 @@ int main(int argc, char **argv) {
     report(name, ms, bytes);
   };
   const bool reg_only = argc > 3 && atoi(argv[3]) == 1;
+  if (argc > 3 && atoi(argv[3]) == 2) {
+    for (int rep = 0; rep < 2; ++rep) {
+      run(probe<Y_NONE>, "base", sb);
+      run(probe<Y_WAVE>, "y.wave", sb + yb);
+      run(probe<Y_XCHG>, "y.xchg", sb + yb);
+      run(probe<Y_SC>, "y.agent", sb + yb);
+      run(probe<Y_NT>, "y.nt", sb + yb);
+    }
+    return 0;
+  }
   for (int rep = 0; rep < 2 && reg_only; ++rep) {
     run(probe<Y_NONE>, "base", sb);
     run(probe<Y_WAVE>, "y.wave", sb + yb);
