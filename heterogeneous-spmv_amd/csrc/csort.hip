@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     const int32_t *__restrict__ vslice, const int32_t *__restrict__ cbase,
     const void *__restrict__ ent, const T *__restrict__ val, const T *__restrict__ x,
     S *__restrict__ part, S *__restrict__ spart, T *__restrict__ y,
-    unsigned long long *__restrict__ trace, int32_t rot_groups) {
+    unsigned long long *__restrict__ trace) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   S *acc = reinterpret_cast<S *>(smem);
   constexpr int NW = kCsortThreads / kWave;
@@ -194,20 +194,9 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
 #endif
   // PF: the next chunk's entries are loaded while this chunk's gathers are
   // in flight (software pipelining across the wave's chunks)
-  // rot_groups > 0 (A/B): the workgroups that share an XCD (b / 8) start
-  // their column sweeps at rot_groups evenly spaced chunks and wrap around,
-  // instead of all sweeping x from its left end at once
-  const int32_t nch = c1 - c0;
-  const int32_t rot = rot_groups > 0 && nch > 0
-                          ? (int32_t)(((int64_t)((b >> 3) % rot_groups) * nch) / rot_groups) : 0;
-  auto chunk_at = [&](int32_t i) {
-    const int32_t j = i + rot;
-    return c0 + (j >= nch ? j - nch : j);
-  };
   if constexpr (PF)
-    if (wid < nch) load_entries<T, U, NT, WIDE>(ent, val, chunk_at(wid), lane, ix, vv);
-  for (int32_t i = wid; i < nch; i += NW) {  // wave-uniform
-    const int32_t c = chunk_at(i);
+    if (c0 + wid < c1) load_entries<T, U, NT, WIDE>(ent, val, c0 + wid, lane, ix, vv);
+  for (int32_t c = c0 + wid; c < c1; c += NW) {  // wave-uniform
     // bit 31 of the chunk base: a "segmented" chunk (see below)
     const uint32_t cb = (uint32_t)wave_uniform(cbase[wave_uniform(c)]);
     const int32_t base = (int32_t)(cb & 0x7fffffffu);
@@ -229,7 +218,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     }
     if constexpr (PF) {
       __builtin_amdgcn_sched_barrier(0);
-      if (i + NW < nch) load_entries<T, U, NT, WIDE>(ent, val, chunk_at(i + NW), lane, ix, vv);
+      if (c + NW < c1) load_entries<T, U, NT, WIDE>(ent, val, c + NW, lane, ix, vv);
       __builtin_amdgcn_sched_barrier(0);
     }
     if (!seg) {
@@ -356,7 +345,7 @@ void launch_csort_main(const DevCsort &c, const T *x, S *part, S *spart, T *y, h
   hipLaunchKernelGGL((hspmv_csort<T, S, U, NT, PF, WIDE>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
                      (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
                      c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y,
-                     c.trace, c.rot_groups);
+                     c.trace);
 }
 
 template <typename T, typename S, int U, bool NT>

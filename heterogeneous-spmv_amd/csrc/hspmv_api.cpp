@@ -189,7 +189,6 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_CSORT_SEG_EXTRA", &t->csort_seg_extra);
   geti("HSPMV_CSORT_TRACE", &t->csort_trace);
   geti("HSPMV_CSORT_LONG", &t->csort_long);
-  geti("HSPMV_CSORT_ROT", &t->csort_rot);
   geti("HSPMV_STREAM_W", &t->stream_waves);
   geti("HSPMV_PLACEMENT", &t->placement_trials);
   geti("HSPMV_CONTIG", &t->contig);
@@ -1406,7 +1405,6 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.row_blocks = (int32_t)NB;
   if (tn.csort_trace == 1 && (rc = dev_alloc(&s.d_cs_trace, 24 * (size_t)G, &s.bytes))) return rc;
   c.trace = s.d_cs_trace;
-  c.rot_groups = std::max(0, tn.csort_rot);
   c.vslice = s.d_cs_vslice;
   c.cbase = s.d_cs_cbase;
   c.ent = s.d_cs_ent;

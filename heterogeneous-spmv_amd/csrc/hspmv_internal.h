@@ -70,7 +70,6 @@ struct Tuning {
   int csort_seg_extra = 0;               // serialised same-slot lanes that flag a chunk (0: default)
   int csort_trace = 0;                   // per-workgroup timestamps (hspmv_diag_csort_trace)
   int csort_long = 0;                    // rows above this many nonzeros are sliced (0: kLongRow)
-  int csort_rot = 0;                     // rotated sweep starts (workgroup groups per XCD; 0 off)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
 };
@@ -103,7 +102,6 @@ struct DevCsort {
   int32_t lds_bytes = 0;
   const int32_t *blk_c = nullptr, *blk_r = nullptr, *blk_v = nullptr, *vslice = nullptr;
   int32_t row_blocks = 0;  // blocks per column part (the parts' own row partitions)
-  int32_t rot_groups = 0;  // A/B: rotated sweep starts per XCD (0: all start left)
   unsigned long long *trace = nullptr;  // diagnostic builds: per-workgroup {start, end, hw_id} (s_memrealtime)
   const int32_t *cbase = nullptr;
   const void *ent = nullptr;  // fp32: {idx, val} records; fp64: idx
