@@ -1,0 +1,440 @@
+// hspmv_csort_build.cpp -- host build of the column-sorted row blocks (csort.hip)
+// (see hspmv_runtime.h for the split of the host runtime).
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstddef>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "hspmv_runtime.h"
+
+namespace hspmv {
+
+// Column-sorted row blocks (csort.hip; the kernel's header says why).
+// Host build: rows are cut into nnz-balanced blocks of at most
+// kCsortMaxSlots - (slices) rows, about one block per CU and column part;
+// every workgroup (block, part) gets the block's nonzeros whose column lies
+// in its part, sorted by column, plus its share of the long-row slices
+// (rows > kLongRow nonzeros, cut per part into kCsortSlice-nonzero slices
+// dealt round-robin over the blocks, each an extra LDS slot).  Entries are
+// padded to whole chunks of 64*U, and a chunk is closed early when its
+// columns would span more than 65535 (16-bit offsets from the chunk base).
+// Padding entries add 0 * x[base] to a dummy slot that is never read.
+// Auto: HBM-resident matrices with irregular gathers and x beyond an XCD's
+// L2 (the x-slab rule, which it replaces: C5 264 -> ~110 us), unless the
+// handle asks for deterministic sums (the slots add in atomic order);
+// HSPMV_KERNEL_CSORT forces it, Tuning.csort = -1 turns auto off,
+// Tuning.csort_parts = 1/2/4 sets the column parts, csort_u = 4/8/16 the
+// chunk.  The row blocks are capped by the device's LDS per workgroup.
+constexpr int32_t kCsortSlice = 2048;
+// a chunk whose instructions would serialise more than this many same-slot
+// lanes in all is stored slot-sorted (segmented)
+constexpr int64_t kCsortSegExtra = 128;
+constexpr int64_t kCsortSegHeavy = 8;  // entries of one row in a chunk that make it a run
+
+struct CsEnt {
+  uint32_t col, slot, k;
+  bool operator<(const CsEnt &o) const {
+    return col != o.col ? col < o.col : (slot != o.slot ? slot < o.slot : k < o.k);
+  }
+};
+
+int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
+                int64_t n, int dtype, unsigned flags) {
+  if (m == 0 || n == 0 || !val) return HSPMV_OK;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s.device) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  int lds_max = 0;  // the row slots must fit one workgroup's LDS on THIS device
+  if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, s.device) != hipSuccess ||
+      lds_max <= 0)
+    return HSPMV_OK;
+  lds_max = std::min(lds_max, kCsortMaxLds);
+  const Tuning &tn = s.tune;
+  if (tn.csort_lds_cap > 0) lds_max = std::min(lds_max, tn.csort_lds_cap);  // A/B
+  const bool slot32 = dtype == HSPMV_F32 && tn.csort_slot32 == 1;
+  const int64_t slot_bytes = slot32 ? 4 : 8;
+  const int32_t max_slots = (int32_t)(lds_max / slot_bytes) - 1;
+  int H = n >= 2 ? 2 : 1;
+  if (tn.csort_parts == 1 || tn.csort_parts == 2 || tn.csort_parts == 4)
+    H = (int)std::min<int64_t>(tn.csort_parts, n);
+  int U = dtype == HSPMV_F32 ? 16 : 8;
+  if (tn.csort_u == 4 || tn.csort_u == 8 || tn.csort_u == 16) U = tn.csort_u;
+  const int bpc = tn.csort_blocks_per_cu > 0 ? std::min(tn.csort_blocks_per_cu, 8) : 1;
+  // 16-byte entry loads: needs U a multiple of 2 (fp32 records) / 4 (fp64 indices)
+  // 16-byte entry loads + the next chunk's entries loaded during this chunk's
+  // gathers: fp32 C5 107 -> 103 us, RCM'd C5 192 -> 190, in four one-process
+  // A/Bs (profiles/r03/ab_c5_wide_pf*.jsonl); fp64 keeps 8-byte loads
+  // (unmeasured).  Neither alone moves C5 (wide 108.8 vs 108.0, PF 109.4).
+  const bool wide_default = dtype == HSPMV_F32;
+  const bool wide = (tn.csort_wide >= 0 ? tn.csort_wide == 1 : wide_default) &&
+                    (dtype == HSPMV_F32 ? U % 2 == 0 : U % 4 == 0);
+  const int64_t C = 64 * U;
+  const size_t sv = dtype_size(dtype);
+  const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX
+                         : (s.tune.csort_long > 0 ? s.tune.csort_long : kLongRow);
+  auto part_of = [&](int64_t c) { return (int)((c * H) / n); };  // c in part floor(c*H/n)
+  // long rows and their slices (per part, kCsortSlice nonzeros each)
+  std::vector<int32_t> lrow, lcs(1, 0);
+  std::vector<std::vector<uint32_t>> slice_k;  // source nonzeros per slice
+  std::vector<int> slice_part;
+  int64_t long_nnz = 0;
+  for (int64_t r = 0; r < m; ++r) {
+    const int32_t k0 = rp[r], k1 = rp[r + 1];
+    if (k1 - k0 <= long_t) continue;
+    long_nnz += k1 - k0;
+    lrow.push_back((int32_t)r);
+    std::vector<std::vector<uint32_t>> byp((size_t)H);
+    for (int32_t k = k0; k < k1; ++k) byp[(size_t)part_of(col[k])].push_back((uint32_t)k);
+    for (int h = 0; h < H; ++h)
+      for (size_t i = 0; i < byp[(size_t)h].size(); i += kCsortSlice) {
+        const size_t e = std::min(byp[(size_t)h].size(), i + kCsortSlice);
+        slice_k.emplace_back(byp[(size_t)h].begin() + (ptrdiff_t)i, byp[(size_t)h].begin() + (ptrdiff_t)e);
+        slice_part.push_back(h);
+      }
+    lcs.push_back((int32_t)slice_k.size());
+  }
+  const int64_t n_slices = (int64_t)slice_k.size();
+  // Row blocks PER COLUMN PART.  Part h is a fixed slice of x,
+  // [ceil(n h / H), ceil(n (h + 1) / H)), and workgroup j works on part
+  // j % H: under round-robin dispatch (workgroup j on XCD j % 8;
+  // tools/xcd_map_probe.hip records it per box) every XCD sweeps one slice,
+  // which its 4 MiB L2 keeps for all its CUs.  Each part has its OWN row
+  // partition, balanced on the nonzeros that fall in that part and capped in
+  // rows (the LDS slots), so the parts' workgroups carry equal work whatever
+  // the ordering: with one row partition for all parts an RCM-ordered
+  // power-law matrix put ~90 % of a block's entries in one part (322 us vs
+  // 108 us on the same matrix unordered), and quantile splits per block, which
+  // balance the work but let every XCD sweep all of x, still took 205 us.
+  const int64_t nb0 = std::max<int64_t>(1, (int64_t)cus * bpc / H);
+  const int64_t reserve = n_slices / nb0 + 2;
+  const int64_t row_cap = max_slots - 1 - reserve;
+  if (row_cap < 64) return HSPMV_OK;  // too many slices for the LDS: not this path
+  std::vector<int32_t> cnt((size_t)(H * m), 0);  // [h][r]: row r's in-kernel nonzeros in part h
+  {
+    const int ntc = (int)std::max<int64_t>(1, std::min<int64_t>(16, m / 65536));
+    std::vector<std::thread> th;
+    for (int t = 0; t < ntc; ++t)
+      th.emplace_back([&, t]() {
+        for (int64_t r = m * t / ntc; r < m * (t + 1) / ntc; ++r) {
+          if (rp[r + 1] - rp[r] > long_t) continue;
+          for (int32_t k = rp[r]; k < rp[r + 1]; ++k) ++cnt[(size_t)(part_of(col[k]) * m + r)];
+        }
+      });
+    for (auto &x : th) x.join();
+  }
+  // Greedy cuts at `target` nonzeros or row_cap rows; the target is the
+  // smallest that yields at most nb0 blocks (one block more would run a
+  // second round of workgroups on one CU and double the launch).
+  auto cut = [&](int h, int64_t target, std::vector<int32_t> *out) -> int64_t {
+    const int32_t *c = cnt.data() + (size_t)h * (size_t)m;
+    int64_t start = 0, acc = 0, nblk = 1;
+    if (out) out->assign(1, 0);
+    for (int64_t r = 0; r < m; ++r) {
+      if (r > start && (r - start >= row_cap || acc >= target)) {
+        if (out) out->push_back((int32_t)r);
+        ++nblk;
+        start = r;
+        acc = 0;
+      }
+      acc += c[r];
+    }
+    if (out) out->push_back((int32_t)m);
+    return nblk;
+  };
+  std::vector<std::vector<int32_t>> brh((size_t)H);
+  int64_t NB = 0;
+  for (int h = 0; h < H; ++h) {
+    int64_t tot_h = 0;
+    for (int64_t r = 0; r < m; ++r) tot_h += cnt[(size_t)(h * m + r)];
+    int64_t lo = std::max<int64_t>(1, (tot_h + nb0 - 1) / nb0), hi = std::max<int64_t>(lo, tot_h + 1);
+    if (cut(h, lo, nullptr) > nb0) {
+      if (cut(h, hi, nullptr) > nb0) lo = hi;  // the row cap alone needs more blocks
+      while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (cut(h, mid, nullptr) <= nb0) hi = mid; else lo = mid + 1;
+      }
+    }
+    cut(h, lo, &brh[(size_t)h]);
+    NB = std::max<int64_t>(NB, (int64_t)brh[(size_t)h].size() - 1);
+  }
+  std::vector<int32_t>().swap(cnt);
+  const int64_t G = NB * H;
+  if (G >= INT32_MAX) return HSPMV_OK;
+  // workgroup j: part j % H, that part's block j / H (empty past its blocks)
+  std::vector<int32_t> wg_rows((size_t)(2 * G), (int32_t)m);
+  for (int64_t j = 0; j < G; ++j) {
+    const auto &b = brh[(size_t)(j % H)];
+    const int64_t i = j / H;
+    if (i + 1 < (int64_t)b.size()) {
+      wg_rows[(size_t)(2 * j)] = b[(size_t)i];
+      wg_rows[(size_t)(2 * j + 1)] = b[(size_t)i + 1];
+    }
+  }
+  // slices dealt round-robin over the blocks of their part
+  std::vector<std::vector<int32_t>> wg_sl((size_t)G);
+  {
+    std::vector<int64_t> next((size_t)H, 0);
+    for (int64_t sl = 0; sl < n_slices; ++sl) {
+      const int h = slice_part[(size_t)sl];
+      const int64_t nbh = (int64_t)brh[(size_t)h].size() - 1;
+      const int64_t i = next[(size_t)h]++ % nbh;
+      wg_sl[(size_t)(i * H + h)].push_back((int32_t)sl);
+    }
+  }
+  // per workgroup: sorted entries, chunk count (pass 1)
+  std::vector<std::vector<CsEnt>> ents((size_t)G);
+  std::vector<int64_t> nchunks((size_t)G, 0);
+  std::vector<int32_t> nslots((size_t)G, 0);
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, G / 4));
+  std::atomic<bool> too_big{false};
+  auto chunk_walk = [&](const std::vector<CsEnt> &E, auto &&emit) {
+    // chunks of C entries, closed early when the span would pass 65535
+    int64_t i = 0, cnt_ = 0;
+    const int64_t ne = (int64_t)E.size();
+    while (i < ne) {
+      const uint32_t c0 = E[(size_t)i].col;
+      int64_t j = i;
+      while (j < ne && j - i < C && E[(size_t)j].col - c0 <= 65535u) ++j;
+      emit(cnt_, c0, i, j);
+      ++cnt_;
+      i = j;
+    }
+    return cnt_;
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+      th.emplace_back([&, t]() {
+        for (int64_t b = t; b < G; b += nt) {
+          const int h = (int)(b % H);
+          const int32_t r0 = wg_rows[(size_t)(2 * b)], r1 = wg_rows[(size_t)(2 * b + 1)];
+          const int32_t nr = r1 - r0;
+          auto &E = ents[(size_t)b];
+          for (int32_t r = r0; r < r1; ++r) {
+            if (rp[r + 1] - rp[r] > long_t) continue;
+            for (int32_t k = rp[r]; k < rp[r + 1]; ++k)
+              if (part_of(col[k]) == h) E.push_back({(uint32_t)col[k], (uint32_t)(r - r0), (uint32_t)k});
+          }
+          const auto &sl = wg_sl[(size_t)b];
+          for (size_t v = 0; v < sl.size(); ++v)
+            for (uint32_t k : slice_k[(size_t)sl[v]])
+              E.push_back({(uint32_t)col[k], (uint32_t)(nr + (int32_t)v), k});
+          std::sort(E.begin(), E.end());
+          nslots[(size_t)b] = nr + (int32_t)sl.size() + 1;  // + the dummy slot
+          if (nslots[(size_t)b] > 65536 || ((int64_t)nslots[(size_t)b] + 1) * slot_bytes > lds_max) too_big = true;
+          nchunks[(size_t)b] = chunk_walk(E, [](int64_t, uint32_t, int64_t, int64_t) {});
+        }
+      });
+    for (auto &x : th) x.join();
+  }
+  if (too_big) return HSPMV_OK;
+  std::vector<int32_t> blk_c((size_t)G + 1, 0), blk_v((size_t)G + 1, 0), vslice;
+  int64_t tot_chunks = 0;
+  int32_t max_slots_used = 1;
+  for (int64_t b = 0; b < G; ++b) {
+    blk_c[(size_t)b] = (int32_t)tot_chunks;
+    tot_chunks += nchunks[(size_t)b];
+    blk_v[(size_t)b] = (int32_t)vslice.size();
+    for (int32_t sl : wg_sl[(size_t)b]) vslice.push_back(sl);
+    max_slots_used = std::max(max_slots_used, nslots[(size_t)b]);
+  }
+  blk_c[(size_t)G] = (int32_t)tot_chunks;
+  blk_v[(size_t)G] = (int32_t)vslice.size();
+  if (tot_chunks * C >= (int64_t)1 << 40 || tot_chunks >= INT32_MAX) return HSPMV_OK;
+  const int64_t tot = tot_chunks * C;
+  // pass 2: the device arrays
+  std::vector<int32_t> cbase((size_t)std::max<int64_t>(tot_chunks, 1), 0);
+  std::vector<uint32_t> idx;
+  std::vector<uint64_t> rec;
+  std::vector<double> val64;
+  if (dtype == HSPMV_F32)
+    rec.assign((size_t)tot, 0);
+  else {
+    idx.assign((size_t)tot, 0);
+    val64.assign((size_t)tot, 0.0);
+  }
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+      th.emplace_back([&, t]() {
+        for (int64_t b = t; b < G; b += nt) {
+          auto &E = ents[(size_t)b];
+          const uint32_t dummy = (uint32_t)(nslots[(size_t)b] - 1);
+          const int64_t cfirst = blk_c[(size_t)b];
+          // entry q of a chunk (lane q % 64, u = q / 64) is stored at q, or,
+          // for 16-byte loads, interleaved so that one load brings the lane
+          // entries u, u+1 (fp32 records, fp64 values) or u..u+3 (fp64 indices)
+          auto at = [&](int64_t q, int per) -> int64_t {
+            if (!wide) return q;
+            const int64_t u = q / 64, lane = q % 64;
+            return (u / per) * (64 * per) + lane * per + (u % per);
+          };
+          std::vector<CsEnt> tmp;
+          uint32_t sl64[64];
+          chunk_walk(E, [&](int64_t ci, uint32_t c0, int64_t i, int64_t j) {
+            const int64_t ch = cfirst + ci;
+            // Same-slot lanes in one instruction serialise the LDS atomics:
+            // an RCM ordering puts a hub row's entries on contiguous columns,
+            // so column order can give one instruction 64 lanes of one row
+            // (RCM power-law: a few workgroups with ~100 K serialised lanes
+            // set the launch's tail, 204 vs 108 us).  Such chunks are stored
+            // sorted by slot instead and flagged (bit 31 of the base): the
+            // kernel sums each instruction's runs first (segmented scan).
+            const CsEnt *src = E.data() + i;
+            bool seg = false;
+            if (tn.csort_seg != 0) {
+              int64_t extra = 0;
+              for (int64_t g = i; g < j; g += 64) {
+                const int64_t e = std::min(j, g + 64);
+                for (int64_t t = g; t < e; ++t) sl64[t - g] = E[(size_t)t].slot;
+                std::sort(sl64, sl64 + (e - g));
+                int run = 1, mx = 1;
+                for (int64_t t = 1; t < e - g; ++t) {
+                  run = sl64[t] == sl64[t - 1] ? run + 1 : 1;
+                  mx = std::max(mx, run);
+                }
+                extra += mx - 1;
+              }
+              const int64_t lim = tn.csort_seg_extra > 0 ? tn.csort_seg_extra : kCsortSegExtra;
+              if (extra > lim || tn.csort_seg == 2) {
+                // the crowded rows (>= kCsortSegHeavy entries in this chunk)
+                // first, slot-sorted, in column order within each: their runs
+                // are contiguous columns (coalesced gathers); the other
+                // entries after them, still in column order
+                std::vector<std::pair<uint32_t, int32_t>> cnt_s;
+                cnt_s.reserve((size_t)(j - i));
+                for (int64_t t = i; t < j; ++t) cnt_s.push_back({E[(size_t)t].slot, 0});
+                std::sort(cnt_s.begin(), cnt_s.end());
+                std::vector<uint32_t> heavy;
+                for (size_t t = 0; t < cnt_s.size();) {
+                  size_t e = t;
+                  while (e < cnt_s.size() && cnt_s[e].first == cnt_s[t].first) ++e;
+                  if ((int64_t)(e - t) >= kCsortSegHeavy || tn.csort_seg == 2) heavy.push_back(cnt_s[t].first);
+                  t = e;
+                }
+                auto is_heavy = [&](uint32_t sl) { return std::binary_search(heavy.begin(), heavy.end(), sl); };
+                tmp.clear();
+                for (int64_t t = i; t < j; ++t)
+                  if (is_heavy(E[(size_t)t].slot)) tmp.push_back(E[(size_t)t]);
+                std::stable_sort(tmp.begin(), tmp.end(), [](const CsEnt &a, const CsEnt &b) { return a.slot < b.slot; });
+                for (int64_t t = i; t < j; ++t)
+                  if (!is_heavy(E[(size_t)t].slot)) tmp.push_back(E[(size_t)t]);
+                src = tmp.data();
+                seg = true;
+              }
+            }
+            cbase[(size_t)ch] = (int32_t)(c0 | (seg ? 0x80000000u : 0u));
+            for (int64_t q = 0; q < C; ++q) {
+              const int64_t o = ch * C + at(q, dtype == HSPMV_F32 ? 2 : 4);
+              const int64_t ov = ch * C + at(q, 2);
+              uint32_t ix = dummy << 16;  // padding: 0 * x[base] into the dummy slot
+              const void *vp = nullptr;
+              if (i + q < j) {
+                const CsEnt &e = src[q];
+                ix = (e.slot << 16) | (e.col - c0);
+                vp = (const char *)val + sv * (size_t)e.k;
+              }
+              if (dtype == HSPMV_F32) {
+                uint32_t vb = 0;
+                if (vp) memcpy(&vb, vp, 4);
+                rec[(size_t)o] = ((uint64_t)vb << 32) | ix;
+              } else {
+                idx[(size_t)o] = ix;
+                if (vp) memcpy(&val64[(size_t)ov], vp, 8);
+              }
+            }
+          });
+          std::vector<CsEnt>().swap(E);
+        }
+      });
+    for (auto &x : th) x.join();
+  }
+  std::vector<uint32_t> mask;
+  if (!lrow.empty()) {
+    mask.assign((size_t)((m + 31) / 32), 0u);
+    for (int32_t r : lrow) mask[(size_t)r >> 5] |= 1u << (r & 31);
+  }
+  int rc;
+  auto up = [&](auto **d, const auto &h) -> int {
+    using E = typename std::decay_t<decltype(h)>::value_type;
+    const size_t bytes = sizeof(E) * std::max<size_t>(h.size(), 1);
+    int r2 = dev_alloc(d, bytes, &s.bytes);
+    if (r2) return r2;
+    if (!h.empty()) HIP_TRY(hipMemcpy(*d, h.data(), sizeof(E) * h.size(), hipMemcpyHostToDevice));
+    return HSPMV_OK;
+  };
+  if ((rc = up(&s.d_cs_blk_c, blk_c)) || (rc = up(&s.d_cs_blk_r, wg_rows)) ||
+      (rc = up(&s.d_cs_blk_v, blk_v)) || (rc = up(&s.d_cs_vslice, vslice)) || (rc = up(&s.d_cs_cbase, cbase)))
+    return rc;
+  if (dtype == HSPMV_F32) {
+    uint64_t *d = nullptr;
+    if ((rc = up(&d, rec))) return rc;
+    s.d_cs_ent = d;
+  } else {
+    uint32_t *di = nullptr;
+    double *dv = nullptr;
+    if ((rc = up(&di, idx))) return rc;
+    s.d_cs_ent = di;
+    if ((rc = up(&dv, val64))) return rc;
+    s.d_cs_val = dv;
+  }
+  const bool direct = H == 1 && lrow.empty();
+  if (!direct) {  // partial sums in the slot type
+    if ((rc = dev_alloc(&s.d_cs_part, slot_bytes * (size_t)H * (size_t)m, &s.bytes))) return rc;
+    if ((rc = dev_alloc(&s.d_cs_spart, slot_bytes * (size_t)std::max<int64_t>(n_slices, 1), &s.bytes)))
+      return rc;
+  }
+  if (!lrow.empty()) {
+    if ((rc = up(&s.d_cs_mask, mask)) || (rc = up(&s.d_cs_long_row, lrow)) || (rc = up(&s.d_cs_long_cs, lcs)))
+      return rc;
+  }
+  // (An in-launch combine -- write-through partials, an arrival counter per
+  // row block, the last arriver adding the parts -- measured slower than
+  // the finishing launch: C5 114.8 vs 107.3 us, profiles/r02s_*.)
+  DevCsort &c = s.csort;
+  c = DevCsort();
+  c.n_wg = (int32_t)G;
+  c.H = H;
+  c.u = U;
+  c.direct = direct ? 1 : 0;
+  c.n_long = (int32_t)lrow.size();
+  c.nontemporal = true;  // the entry stream is read once; keep x in the caches
+  if (tn.csort_nt >= 0) c.nontemporal = tn.csort_nt != 0;  // A/B knobs
+  c.prefetch = wide && dtype == HSPMV_F32;  // see `wide` above
+  if (tn.csort_pf >= 0) c.prefetch = tn.csort_pf != 0;
+  c.slot32 = slot32;
+  c.wide = wide;
+  c.m = m;
+  c.lds_bytes = (int32_t)(slot_bytes * max_slots_used);
+  c.blk_c = s.d_cs_blk_c;
+  c.blk_r = s.d_cs_blk_r;
+  c.blk_v = s.d_cs_blk_v;
+  c.row_blocks = (int32_t)NB;
+  if (tn.csort_trace == 1 && (rc = dev_alloc(&s.d_cs_trace, 24 * (size_t)G, &s.bytes))) return rc;
+  c.trace = s.d_cs_trace;
+  c.vslice = s.d_cs_vslice;
+  c.cbase = s.d_cs_cbase;
+  c.ent = s.d_cs_ent;
+  c.val = s.d_cs_val;
+  c.part = s.d_cs_part;
+  c.spart = s.d_cs_spart;
+  c.long_mask = s.d_cs_mask;
+  c.long_row = s.d_cs_long_row;
+  c.long_cs = s.d_cs_long_cs;
+  // bytes moved: the entry stream + chunk bases + x (distinct columns) + the
+  // partial sums written and read back + y
+  const double xb = (double)s.x_entries * (double)sv;
+  s.csort_format_bytes = (double)tot * (double)(4 + sv) + 4.0 * (double)tot_chunks + xb +
+                         (direct ? 0.0 : 2.0 * (double)slot_bytes * ((double)H * (double)m + (double)n_slices)) +
+                         (double)sv * (double)m;
+  s.A.has_csort = true;
+  return HSPMV_OK;
+}
+
+}  // namespace hspmv

@@ -5,7 +5,7 @@
 set -o pipefail
 TAG=${1:-ystore}
 R=$GRAFT_REPO_ROOT; D=$R/gpurun_out/$TAG; mkdir -p $D
-B=$R/heterogeneous-spmv_amd/build/bw_probe6
+B=$R/heterogeneous-spmv_amd/build/probes/bw_probe6
 cd /tmp && export TMPDIR=/tmp
 P=(
  "TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_TD_TCP_STALL_CYCLES_sum"

@@ -1,10 +1,10 @@
 # GPU-box pass: the texture-data (TD) cost of register loads, LDS-DMA loads
-# and C5-like gathers (tools/td_probe.hip), plain, then TD/TCP counters.
+# and C5-like gathers (tools/probes/td_probe.hip), plain, then TD/TCP counters.
 # Usage (from the repo root): bash heterogeneous-spmv_amd/tools/gpu_td_probe.sh TAG
 set -o pipefail
 TAG=${1:-td}
 R=$GRAFT_REPO_ROOT; D=$R/gpurun_out/$TAG; mkdir -p $D
-B=$R/heterogeneous-spmv_amd/build/td_probe
+B=$R/heterogeneous-spmv_amd/build/probes/td_probe
 timeout -k 10 120 $B > $D/td.jsonl 2> $D/td.err || { cat $D/td.err; exit 1; }
 cat $D/td.jsonl
 cd /tmp && export TMPDIR=/tmp

@@ -24,6 +24,6 @@ mkdir -p "$(dirname "$O")"
 } > "$O" 2>&1
 echo "host info -> $O"
 B=$(dirname "$0")/../build
-if [ -x $B/xcd_map_probe ]; then
-  { echo "== workgroup -> XCD mapping (tools/xcd_map_probe.hip)"; timeout -k 5 60 $B/xcd_map_probe 2048 256; timeout -k 5 60 $B/xcd_map_probe 256 1024; } >> "$O" 2>&1
+if [ -x $B/probes/xcd_map_probe ]; then
+  { echo "== workgroup -> XCD mapping (tools/xcd_map_probe.hip)"; timeout -k 5 60 $B/probes/xcd_map_probe 2048 256; timeout -k 5 60 $B/probes/xcd_map_probe 256 1024; } >> "$O" 2>&1
 fi
