@@ -635,7 +635,7 @@ def main():
                        "csr3_maps": ({"n_ssr": maps.n_ssr, "n_sr": maps.n_sr} if maps is not None
                                      else None),
                        "kernel": info["kernel_name"], "chunk_u": info["chunk_u"],
-                       "csr3_plan": {0: None, 1: "aligned", 2: "packed", 3: "ssr"}[info["csr3_plan"]],
+                       "csr3_plan": hspmv._lib.CSR3_PLAN_NAMES[info["csr3_plan"]],
                        "deterministic": bool(info["deterministic"]),
                        "xcd_chunk": info["xcd_remap"],
                        "x_dict": info["x_dict"], "x_windows": info["x_windows"],

@@ -219,7 +219,7 @@ inline int run_and_report(const hspmv_csr_buf &A, const hspmv_csr3_buf *maps, in
   hspmv_timing t;
   if (hspmv_run(h, 5, num_runs, &t) != HSPMV_OK) return die("hspmv_run");
   hspmv_info info;
-  hspmv_get_info(h, &info);
+  hspmv_get_info_sized(h, &info, sizeof(info));
   printf("TimeMin: %lg\n", t.wall_min);
   printf("TimeMax: %lg\n", t.wall_max);
   printf("TimeAvg: %lg\n", t.wall_avg);

@@ -108,6 +108,7 @@ int create_single(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *
     free_shard(s, h->borrowed);
     return rc;
   }
+  (void)ncclGetVersion(&h->rccl_version);
   *hp = h.release();
   return HSPMV_OK;
 }
@@ -126,6 +127,15 @@ int check_devices(const int *devices, int n, int *ndev_out) {
 }  // namespace
 
 extern "C" {
+
+int hspmv_rccl_version(int *version) {
+  clear_error();
+  if (!version) return set_error(HSPMV_E_INVALID, "NULL argument");
+  *version = 0;
+  ncclResult_t r = ncclGetVersion(version);
+  if (r != ncclSuccess) return set_error(HSPMV_E_RCCL, "ncclGetVersion: %s", ncclGetErrorString(r));
+  return HSPMV_OK;
+}
 
 int hspmv_device_count(int *count) {
   clear_error();
@@ -372,8 +382,10 @@ int hspmv_exchange(hspmv_handle *h, double *bcast_s, double *gather_s) {
   return HSPMV_OK;
 }
 
-int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
-  clear_error();
+}  // extern "C"
+
+// The full report (this header's hspmv_info).
+static int fill_info(hspmv_handle *h, hspmv_info *out) {
   int rc;
   if ((rc = check_handle(h))) return rc;
   if (!out) return set_error(HSPMV_E_INVALID, "NULL output");
@@ -408,11 +420,31 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   for (size_t k = 0; k < s.place_us.size() && k < 8; ++k) out->placement_us[k] = s.place_us[k];
   out->deterministic = 1;
   for (auto &sh : h->shards) out->deterministic &= sh.plan.kernel == kCsort ? 0 : 1;
+  // the maps-driven plans need maps; a CSR matrix whose heavy 64-row groups
+  // sent it to the CSR3 kernel runs build_tasks' row groups
   out->csr3_plan = s.plan.kernel != kCsr3 ? 0
+                   : s.A.n_ssr == 0 ? HSPMV_CSR3_PLAN_ROW_GROUPS
                    : s.h_tasks.empty() ? HSPMV_CSR3_PLAN_SSR
                    : csr3_fill(s.tune) ? HSPMV_CSR3_PLAN_ALIGNED : HSPMV_CSR3_PLAN_PACKED;
   out->csort_slot_bytes = s.plan.kernel == kCsort ? (s.dp.cs.slot32 ? 4 : 8) : 0;
   out->csort_row_blocks = s.plan.kernel == kCsort ? s.dp.cs.row_blocks : 0;
+  out->rccl_version = h->rccl_version;
+  for (auto &sh : h->shards)
+    if (sh.plan.kernel == kCsort) {
+      out->csort_chunks += sh.csort_chunks;
+      out->csort_seg_chunks += sh.csort_seg_chunks;
+    }
+  return HSPMV_OK;
+}
+
+extern "C" {
+
+int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
+  clear_error();
+  hspmv_info full;
+  int rc = fill_info(h, &full);
+  if (rc) return rc;
+  memcpy(out, &full, offsetof(hspmv_info, deterministic));  // the 0.1 layout
   return HSPMV_OK;
 }
 
@@ -437,7 +469,7 @@ int hspmv_get_info_sized(hspmv_handle *h, hspmv_info *out, uint32_t out_size) {
   clear_error();
   if (!out) return set_error(HSPMV_E_INVALID, "NULL output");
   hspmv_info full;
-  int rc = hspmv_get_info(h, &full);
+  int rc = fill_info(h, &full);
   if (rc) return rc;
   memcpy(out, &full, std::min<size_t>(out_size, sizeof(full)));
   return HSPMV_OK;

@@ -259,6 +259,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     idx.assign((size_t)tot, 0);
     val64.assign((size_t)tot, 0.0);
   }
+  std::atomic<int64_t> n_seg{0};  // chunks stored slot-sorted (segmented)
   {
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t)
@@ -327,6 +328,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
                   if (!is_heavy(E[(size_t)t].slot)) tmp.push_back(E[(size_t)t]);
                 src = tmp.data();
                 seg = true;
+                n_seg.fetch_add(1, std::memory_order_relaxed);
               }
             }
             cbase[(size_t)ch] = (int32_t)(c0 | (seg ? 0x80000000u : 0u));
@@ -416,6 +418,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.blk_r = s.d_cs_blk_r;
   c.blk_v = s.d_cs_blk_v;
   c.row_blocks = (int32_t)NB;
+  s.csort_seg_chunks = n_seg.load();
+  s.csort_chunks = tot_chunks;
   if (tn.csort_trace == 1 && (rc = dev_alloc(&s.d_cs_trace, 24 * (size_t)G, &s.bytes))) return rc;
   c.trace = s.d_cs_trace;
   c.vslice = s.d_cs_vslice;

@@ -232,7 +232,7 @@ extern "C" {
 
 const char *hspmv_last_error(void) { return g_err.c_str(); }
 
-const char *hspmv_version(void) { return "hspmv 0.1 (gfx950)"; }
+const char *hspmv_version(void) { return "hspmv 0.3 (gfx950)"; }
 
 void hspmv_free_csr(hspmv_csr_buf *A) {
   if (!A) return;

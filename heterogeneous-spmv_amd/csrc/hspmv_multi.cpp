@@ -86,6 +86,7 @@ int create_sharded(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps 
     }
   }
   h->sharded = true;
+  (void)ncclGetVersion(&h->rccl_version);
   *hp = h.release();
   return HSPMV_OK;
 }

@@ -30,8 +30,9 @@ int tuning_from_options(const hspmv_options *o, Tuning *t) {
       (v.stream_waves && v.stream_waves != 1 && v.stream_waves != 2 && v.stream_waves != 4) ||
       v.task_nnz < 0 || v.x_dict_cap < 0 || v.placement_trials < 0 || v.placement_trials > 8)
     return set_error(HSPMV_E_INVALID, "hspmv_options: value out of range");
-  if (v.deterministic && (v.flags & 0xFu) == kCsort)
-    return set_error(HSPMV_E_INVALID, "HSPMV_KERNEL_CSORT is not deterministic");
+  if (v.deterministic && ((v.flags & 0xFu) == kCsort || v.csort > 0))
+    return set_error(HSPMV_E_INVALID, "the column-sorted kernel (HSPMV_KERNEL_CSORT, csort = 1) "
+                                      "is not deterministic");
   t->csr3_plan = v.csr3_plan;
   t->task_nnz = v.task_nnz;
   t->x_windows = v.x_windows < 0 ? -1 : 0;

@@ -72,6 +72,7 @@ struct Shard {
   double *d_cs_part = nullptr, *d_cs_spart = nullptr;
   DevCsort csort;
   double csort_format_bytes = 0.0;   // bytes one csort SpMV moves
+  int64_t csort_chunks = 0, csort_seg_chunks = 0;  // chunks, and those stored slot-sorted
   int c16g_shape = 0;                // group-base columns built for kStream groups / kCsr3 tasks
   std::vector<int32_t> h_xwin;       // built at upload (host columns at hand)
   std::vector<int32_t> h_xwin_t;     // the same per packed CSR-3 task
@@ -116,6 +117,7 @@ struct hspmv_handle {
     return t;
   }
   std::vector<ncclComm_t> comms;
+  int rccl_version = 0;   // ncclGetVersion of the RCCL this process resolved
 };
 
 namespace hspmv {

@@ -493,7 +493,9 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
     const int cm = s.tune.csort;  // -1 off, 0 auto, 1 whenever it can be built
     const double sv = (double)dtype_size(dtype);
     const double footprint = (double)rp[m] * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv;
-    bool want = kf == kCsort || cm == 1;
+    // a deterministic handle never builds the csort tables: the planner
+    // would pick kCsort whenever they exist (plan_launch)
+    bool want = !s.tune.deterministic && (kf == kCsort || cm == 1);
     if (!want && kf == kAuto && cm == 0 && !s.tune.deterministic && s.tune.x_slabs == 0 &&
         footprint > kMallResident && (double)n * sv > 4.0 * 1024 * 1024)
       want = irregular_gathers(rp, col, m, sv);

@@ -288,9 +288,9 @@ using namespace hspmv;
 
 extern "C" {
 
-int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, const hspmv_options *opt,
-                     int64_t cap_entries, int64_t *n_blocks, int64_t *n_records, int32_t *blk,
-                     int32_t *runs, uint16_t *pos) {
+int hspmv_xdict_plan_ex(const hspmv_csr *A, const hspmv_csr3_maps *maps, const hspmv_options *opt,
+                        int64_t cap_entries, int64_t *n_blocks, int64_t *n_records, int32_t *blk,
+                        int32_t *runs, uint16_t *pos) {
   clear_error();
   if (!n_blocks || !n_records) return set_error(HSPMV_E_INVALID, "NULL output");
   *n_blocks = 0;
@@ -325,6 +325,16 @@ int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, const hspm
   if (runs) memcpy(runs, P.rec.data(), 4 * P.rec.size());
   if (pos && A->nnz) memcpy(pos, P.pos.data(), 2 * (size_t)A->nnz);
   return HSPMV_OK;
+}
+
+int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, unsigned flags,
+                     int64_t cap_entries, int64_t *n_blocks, int64_t *n_records, int32_t *blk,
+                     int32_t *runs, uint16_t *pos) {
+  hspmv_options o;
+  memset(&o, 0, sizeof(o));
+  o.struct_size = sizeof(o);
+  o.flags = flags;
+  return hspmv_xdict_plan_ex(A, maps, &o, cap_entries, n_blocks, n_records, blk, runs, pos);
 }
 
 }  // extern "C"

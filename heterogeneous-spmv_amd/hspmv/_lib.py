@@ -116,10 +116,13 @@ class Info(C.Structure):
                 ("placement_trials", C.c_int32), ("placement_pick", C.c_int32),
                 ("placement_us", C.c_double * 8),
                 ("deterministic", C.c_int32), ("csr3_plan", C.c_int32),
-                ("csort_slot_bytes", C.c_int32), ("csort_row_blocks", C.c_int32)]
+                ("csort_slot_bytes", C.c_int32), ("csort_row_blocks", C.c_int32),
+                ("rccl_version", C.c_int32), ("reserved0", C.c_int32),
+                ("csort_chunks", C.c_int64), ("csort_seg_chunks", C.c_int64)]
 
 
 CSR3_PLANS = {"auto": 0, "aligned": 1, "packed": 2, "ssr": 3}
+CSR3_PLAN_NAMES = {0: None, 1: "aligned", 2: "packed", 3: "ssr", 4: "row_groups"}
 
 
 class Options(C.Structure):
@@ -201,10 +204,13 @@ SIGNATURES = {
                                          C.POINTER(Csr3Buf), _P]),
     "hspmv_csr3_params": (C.c_int, [C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hspmv_partition_rows": (C.c_int, [C.c_int64, _P, C.POINTER(Csr3Maps), C.c_int, _P]),
-    "hspmv_xdict_plan": (C.c_int, [C.POINTER(Csr), C.POINTER(Csr3Maps), C.POINTER(Options), C.c_int64,
+    "hspmv_xdict_plan_ex": (C.c_int, [C.POINTER(Csr), C.POINTER(Csr3Maps), C.POINTER(Options), C.c_int64,
+                                      C.POINTER(C.c_int64), C.POINTER(C.c_int64), _P, _P, _P]),
+    "hspmv_xdict_plan": (C.c_int, [C.POINTER(Csr), C.POINTER(Csr3Maps), C.c_uint, C.c_int64,
                                    C.POINTER(C.c_int64), C.POINTER(C.c_int64), _P, _P, _P]),
     "hspmv_alg_bytes": (C.c_double, [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int64]),
     "hspmv_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "hspmv_rccl_version": (C.c_int, [C.POINTER(C.c_int)]),
     "hspmv_last_error": (C.c_char_p, []),
     "hspmv_version": (C.c_char_p, []),
 }

@@ -256,7 +256,7 @@ def partition_rows(row_ptr: np.ndarray, parts: int, maps: Optional[Csr3Maps] = N
 
 def xdict_plan(A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, kernel: str = "auto",
                cap_entries: int = 0, split: bool = True, options: Optional[dict] = None):
-    """Block x dictionaries the library would build for A (hspmv_xdict_plan):
+    """Block x dictionaries the library would build for A (hspmv_xdict_plan_ex):
     (blk, runs, pos) with runs as an (n_records, 2) array of {x_start,
     lds_off}, or None when some workgroup exceeds cap_entries (0 = the
     library's LDS cap for A's dtype)."""
@@ -267,13 +267,13 @@ def xdict_plan(A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, kernel: str = "
     nb, nr = C.c_int64(), C.c_int64()
     L = lib()
     args = (C.byref(cs), C.byref(ms) if ms is not None else None, C.byref(opt), int(cap_entries))
-    check(L.hspmv_xdict_plan(*args, C.byref(nb), C.byref(nr), None, None, None), "xdict_plan")
+    check(L.hspmv_xdict_plan_ex(*args, C.byref(nb), C.byref(nr), None, None, None), "xdict_plan")
     if nb.value == 0:
         return None
     blk = np.empty(nb.value + 1, np.int32)
     runs = np.empty((nr.value, 2), np.int32)
     pos = np.zeros(max(A.nnz, 1), np.uint16)
-    check(L.hspmv_xdict_plan(*args, C.byref(nb), C.byref(nr), _ptr(blk), _ptr(runs), _ptr(pos)),
+    check(L.hspmv_xdict_plan_ex(*args, C.byref(nb), C.byref(nr), _ptr(blk), _ptr(runs), _ptr(pos)),
           "xdict_plan")
     return blk, runs, pos[:A.nnz]
 
@@ -331,7 +331,11 @@ class SpMV:
         h = C.c_void_p()
         if options:  # explicit planner choices: hspmv_create_ex
             if num_gpus != 1 and devices is None:
-                devices = list(range(num_gpus))
+                # num_gpus <= 0 means every visible GPU, as in hspmv_create
+                n = num_gpus if num_gpus > 0 else device_count()
+                if n < 1:
+                    raise HspmvError("hspmv_create_ex", -6, "no HIP device visible")
+                devices = list(range(n))
             opt = _lib.make_options(flags, options, device=0 if device is None else device,
                                     stream=stream, devices=devices)
             rc = lib().hspmv_create_ex(C.byref(h), C.byref(cs),
@@ -427,7 +431,7 @@ class SpMV:
     @property
     def info(self) -> dict:
         i = _lib.Info()
-        check(lib().hspmv_get_info(self._h, C.byref(i)), "hspmv_get_info")
+        check(lib().hspmv_get_info_sized(self._h, C.byref(i), C.sizeof(i)), "hspmv_get_info_sized")
         d = {k: getattr(i, k) for k, _ in _lib.Info._fields_}
         d["placement_us"] = [round(v, 3) for v in d["placement_us"][:d["placement_trials"]]]
         d["kernel_name"] = KERNEL_NAMES.get(d["kernel"], "?")

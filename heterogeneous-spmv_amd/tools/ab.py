@@ -76,7 +76,7 @@ def main():
             assert L.hspmv_set_x(h, x.ctypes.data) == 0
             hs.append(h)
             inf = _lib.Info()
-            assert L.hspmv_get_info(h, C.byref(inf)) == 0
+            assert L.hspmv_get_info_sized(h, C.byref(inf), C.sizeof(inf)) == 0
             places.append([round(v, 2) for v in inf.placement_us[:inf.placement_trials]] +
                           ([f"pick {inf.placement_pick}"] if inf.placement_trials else []))
         ys = []

@@ -107,7 +107,7 @@ int main(int argc, char **argv) {
   hspmv_bind_x_device(h, d_x);
   hspmv_bind_y_device(h, d_y2);
   hspmv_info info;
-  hspmv_get_info(h, &info);
+  hspmv_get_info_sized(h, &info, sizeof(info));
   const double alg = info.alg_bytes;
 
   hipsparseHandle_t sp;

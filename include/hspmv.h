@@ -35,7 +35,10 @@ extern "C" {
 #endif
 
 #define HSPMV_VERSION_MAJOR 0
-#define HSPMV_VERSION_MINOR 2  /* 0.2: hspmv_options, info.deterministic */
+#define HSPMV_VERSION_MINOR 3  /* 0.2: hspmv_options, info.deterministic;
+                                  0.3: info.rccl_version / csort chunks,
+                                  hspmv_get_info fills the 0.1 layout only,
+                                  hspmv_xdict_plan_ex, hspmv_rccl_version */
 
 /* ---------------------------------------------------------------- status */
 #define HSPMV_OK 0
@@ -160,6 +163,15 @@ typedef struct {
   int32_t csort_slot_bytes; /* CSORT: LDS row-slot width (8 = fp64 sums)    */
   int32_t csort_row_blocks; /* CSORT: row blocks per column part (each part
                                has its own nnz-balanced row partition)     */
+  /* since 0.3 */
+  int32_t rccl_version;     /* ncclGetVersion() of the RCCL this process
+                               resolved (librccl.so.1 is one SONAME for the
+                               ROCm and the PyTorch copy: the first loaded
+                               wins), e.g. 22703 = 2.27.3                   */
+  int32_t reserved0;
+  int64_t csort_chunks;     /* CSORT: 64*U-entry chunks of the launch       */
+  int64_t csort_seg_chunks; /* CSORT: of those, chunks stored slot-sorted
+                               (crowded rows summed by a segmented scan)   */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
@@ -250,6 +262,9 @@ typedef struct hspmv_handle hspmv_handle;
                                      map), its super-rows split over W waves
                                      by nonzeros: the reference's cuSpMV_3
                                      mapping (csrk.cu:245-319)               */
+#define HSPMV_CSR3_PLAN_ROW_GROUPS 4 /* hspmv_info only: a CSR matrix (no
+                                     maps) run by the CSR3 kernel over 64-row
+                                     groups with the heavy ones cut         */
 typedef struct {
   uint32_t struct_size;   /* sizeof(hspmv_options) of the caller            */
   uint32_t flags;         /* HSPMV_KERNEL_* | HSPMV_FLAG_* (hspmv_create)    */
@@ -343,9 +358,12 @@ int hspmv_get_y(hspmv_handle *h, void *y_host);
  * every GPU's full-length buffer, timed (seconds).  Either pointer may be NULL. */
 int hspmv_exchange(hspmv_handle *h, double *bcast_x_s, double *gather_y_s);
 
+/* Fills the 0.1 layout of hspmv_info only (every field before
+ * `deterministic`), so a caller built against any header gets no write past
+ * its struct.  The fields since 0.2 come from hspmv_get_info_sized. */
 int hspmv_get_info(hspmv_handle *h, hspmv_info *out);
-/* The same for a caller whose hspmv_info may be older (shorter) than this
- * library's: fills min(out_size, sizeof(hspmv_info)) bytes. */
+/* Fills min(out_size, sizeof(hspmv_info)) bytes: pass sizeof(hspmv_info) of
+ * the header you were built against. */
 int hspmv_get_info_sized(hspmv_handle *h, hspmv_info *out, uint32_t out_size);
 void hspmv_destroy(hspmv_handle *h);
 
@@ -428,12 +446,19 @@ int hspmv_partition_rows(int64_t m, const int32_t *row_ptr,
  * cap_entries (<= 0: the library's LDS cap for A's dtype), so no dictionary.
  * opt (NULL = defaults) supplies the kernel flags and the CSR-3 plan.
  * Not a reference interface: the test and diagnostic view of the format. */
-int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, const hspmv_options *opt,
+int hspmv_xdict_plan_ex(const hspmv_csr *A, const hspmv_csr3_maps *maps, const hspmv_options *opt,
+                        int64_t cap_entries, int64_t *n_blocks, int64_t *n_records,
+                        int32_t *blk, int32_t *runs, uint16_t *pos);
+/* The 0.1 form: kernel flags instead of options (= hspmv_xdict_plan_ex with
+ * an hspmv_options holding only these flags). */
+int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, unsigned flags,
                      int64_t cap_entries, int64_t *n_blocks, int64_t *n_records,
                      int32_t *blk, int32_t *runs, uint16_t *pos);
 double hspmv_alg_bytes(int64_t m, int64_t n, int64_t nnz, int dtype,
                        int64_t n_ssr, int64_t n_sr);
 int hspmv_device_count(int *count);
+/* ncclGetVersion() of the RCCL this process resolved (no device needed). */
+int hspmv_rccl_version(int *version);
 const char *hspmv_last_error(void);
 const char *hspmv_version(void);
 

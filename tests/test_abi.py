@@ -88,3 +88,25 @@ def test_struct_layouts_match_the_header(tmp_path):
         assert got[(cname, "size")] == ctypes.sizeof(py), cname
         for f, _ in py._fields_:
             assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+
+
+def test_rccl_version_is_the_resolved_librccl():
+    """hspmv_rccl_version (and hspmv_info.rccl_version on every handle)
+    report ncclGetVersion() of the RCCL this process resolved: librccl.so.1
+    is one SONAME for the ROCm and the PyTorch copy, so the first one
+    loaded serves both."""
+    v = ctypes.c_int()
+    assert hspmv.lib().hspmv_rccl_version(ctypes.byref(v)) == 0
+    assert v.value >= 21800  # RCCL 2.18 or newer: MAJOR*10000 + MINOR*100 + PATCH
+    assert hspmv.lib().hspmv_rccl_version(None) == -1
+    assert "rccl_version" in dict(_lib.Info._fields_)
+
+
+def test_get_info_fills_only_the_0_1_layout():
+    """hspmv_get_info never writes past the 0.1 struct (fields before
+    `deterministic`), so an old caller cannot be overrun; the newer fields
+    come from hspmv_get_info_sized.  Checked on the header offsets."""
+    text = _lib.HEADER.read_text()
+    assert "#define HSPMV_VERSION_MINOR 3" in text
+    assert _lib.Info.deterministic.offset < ctypes.sizeof(_lib.Info)
+    assert _lib.Info.rccl_version.offset > _lib.Info.csort_row_blocks.offset

@@ -158,6 +158,10 @@ def test_csort_run_to_run_fp64_and_deterministic_option():
     assert fp64_tol_ok(yd[0], y64, absrow)
     with pytest.raises(hspmv.HspmvError):
         hspmv.SpMV(A, kernel="csort", options={"deterministic": 1})
+    # the csort option asks for the same kernel: refused together with
+    # deterministic too (the tables, once built, would be picked)
+    with pytest.raises(hspmv.HspmvError):
+        hspmv.SpMV(A, options={"csort": 1, "deterministic": 1})
 
 
 def _hub_rows(seed=5, m=40_000, n=400_000):
@@ -188,7 +192,14 @@ def test_csort_segmented_chunks_for_contiguous_hub_rows(dtype):
     for parts in (1, 2):
         y, info = run(A, x, kernel="csort", options={"csort_parts": parts})
         assert info["kernel_name"] == "csort" and info["csort_row_blocks"] > 0
+        # the hub rows' chunks really were stored slot-sorted (the segmented
+        # scan ran), and only those: most chunks stay in column order
+        assert 0 < info["csort_seg_chunks"] < info["csort_chunks"] // 2, info
         check(A, x, y)
+    # random columns: no instruction crowds one slot, no segmented chunk
+    B = gen.powerlaw(60_000, seed=5, dtype=dtype)
+    y, info = run(B, gen.rand_x(B.n, 3).astype(dtype), kernel="csort")
+    assert info["csort_chunks"] > 0 and info["csort_seg_chunks"] == 0
 
 
 def test_csort_rcm_powerlaw_matches_oracle():

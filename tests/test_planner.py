@@ -59,6 +59,8 @@ def test_mid_density_band(per_row):
     assert info["deterministic"] == 1
     # a 64-row group of > 2048 nonzeros is a heavy group: CSR3 wave tasks
     assert (info["kernel_name"] == "csr3") == (64 * per_row > 2048)
+    # no maps: the CSR3 kernel runs the cut 64-row groups, reported as such
+    assert info["csr3_plan"] == (4 if info["kernel_name"] == "csr3" else 0)
     check(A, x, y, info)
     maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(per_row, "volta"))
     y3, i3 = run(A, x, maps)

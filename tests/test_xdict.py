@@ -195,3 +195,33 @@ def test_stencil_reuse():
     assert entries < 0.35 * A.nnz
     nruns = np.diff(blk) - 1
     assert nruns.mean() < 12
+
+
+def test_0_1_signature_equals_ex():
+    """hspmv_xdict_plan keeps its 0.1 signature (kernel flags as the third
+    argument) and plans exactly what hspmv_xdict_plan_ex plans with those
+    flags in an hspmv_options."""
+    import ctypes as C
+    from hspmv import _lib
+    A = gen.stencil27(12)
+    cs = A.c_struct()
+    res = []
+    for ex in (False, True):
+        nb, nr = C.c_int64(), C.c_int64()
+        if ex:
+            opt = _lib.make_options(_lib.KERNEL_STREAM, None)
+            third = C.byref(opt)
+            fn = hspmv.lib().hspmv_xdict_plan_ex
+        else:
+            third = _lib.KERNEL_STREAM
+            fn = hspmv.lib().hspmv_xdict_plan
+        assert fn(C.byref(cs), None, third, 0, C.byref(nb), C.byref(nr), None, None, None) == 0
+        blk = np.empty(nb.value + 1, np.int32)
+        runs = np.empty((nr.value, 2), np.int32)
+        pos = np.zeros(A.nnz, np.uint16)
+        assert fn(C.byref(cs), None, third, 0, C.byref(nb), C.byref(nr), blk.ctypes.data,
+                  runs.ctypes.data, pos.ctypes.data) == 0
+        res.append((blk, runs, pos))
+    assert res[0][0].size > 1
+    for a, b in zip(*res):
+        assert np.array_equal(a, b)
