@@ -170,6 +170,43 @@ def set_schedule(kind: str = "static", threads: int = 0) -> None:
     lib().orc_set_threads(int(threads))
 
 
+def time_spmv_samples(row_ptr, col_idx, val, x, warmup: int = 5, runs: int = 20) -> np.ndarray:
+    """The same protocol, every run's seconds (for the median)."""
+    rp, ci, val, x = _prep(row_ptr, col_idx, val, x)
+    y = np.zeros(rp.shape[0] - 1, val.dtype)
+    out = np.zeros(int(runs), np.float64)
+    L = lib()
+    fn = L.orc_time_omp_spmv_samples_f64 if val.dtype == np.float64 else L.orc_time_omp_spmv_samples_f32
+    fn.argtypes = [_i64, _p, _p, _p, _p, _p, C.c_int, C.c_int, _p]
+    fn(rp.shape[0] - 1, _c(rp), _c(ci), _c(val), _c(x), _c(y), int(warmup), int(runs), _c(out))
+    return out
+
+
+def bind_threads(nthreads: int, places: list) -> int:
+    """Team thread t -> CPU set places[t % len(places)] (orc_bind_threads);
+    returns the threads bound."""
+    off = np.zeros(len(places) + 1, np.int32)
+    off[1:] = np.cumsum([len(p) for p in places])
+    cpus = np.array([c for p in places for c in p] or [0], np.int32)
+    L = lib()
+    L.orc_bind_threads.argtypes = [C.c_int, C.c_int, _p, _p]
+    return int(L.orc_bind_threads(int(nthreads), len(places), _c(off), _c(cpus)))
+
+
+def localize(row_ptr, col_idx, val):
+    """First-touch copies of a CSR in omp_spmv's static row partition
+    (orc_localize_csr): each team thread's rows on its own NUMA node."""
+    rp = np.ascontiguousarray(row_ptr, np.int32)
+    ci = np.ascontiguousarray(col_idx, np.int32)
+    val = np.ascontiguousarray(val)
+    rp2, ci2, v2 = np.empty_like(rp), np.empty_like(ci), np.empty_like(val)  # untouched pages
+    L = lib()
+    L.orc_localize_csr.argtypes = [_i64, _p, _p, _p, C.c_int, _p, _p, _p]
+    L.orc_localize_csr(rp.shape[0] - 1, _c(rp), _c(ci), _c(val), val.itemsize, _c(rp2), _c(ci2),
+                       _c(v2))
+    return rp2, ci2, v2
+
+
 def time_spmv(row_ptr, col_idx, val, x, warmup: int = 5, runs: int = 20):
     """OpenMP omp_spmv timed like spmv-csr/spmv.c:164-185 -> (tmin, tmax, tavg, threads)."""
     rp, ci, val, x = _prep(row_ptr, col_idx, val, x)

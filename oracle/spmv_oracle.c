@@ -16,8 +16,10 @@
  * product rounded then sum rounded (no FMA contraction: built with
  * -ffp-contract=off, exactly what gcc emits for the reference on x86-64).
  */
+#define _GNU_SOURCE
 #include <math.h>
 #include <omp.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -390,6 +392,72 @@ int orc_time_omp_spmv_f32(int64_t m, const int32_t *rp, const int32_t *ci,
   }
   *tmin = mn; *tmax = mx; *tavg = runs ? sum / runs : 0.0;
   return 0;
+}
+
+/* The same protocol keeping every run's time (seconds) in samples[runs],
+ * so the caller can report the median beside TimeMin/TimeAvg. */
+int orc_time_omp_spmv_samples_f64(int64_t m, const int32_t *rp, const int32_t *ci,
+                                  const double *val, const double *x, double *y,
+                                  int warmup, int runs, double *samples) {
+  for (int i = 0; i < warmup; ++i) orc_omp_spmv_f64(m, rp, ci, val, x, y);
+  for (int i = 0; i < runs; ++i) {
+    double tic = omp_get_wtime();
+    orc_omp_spmv_f64(m, rp, ci, val, x, y);
+    samples[i] = omp_get_wtime() - tic;
+  }
+  return 0;
+}
+
+int orc_time_omp_spmv_samples_f32(int64_t m, const int32_t *rp, const int32_t *ci,
+                                  const float *val, const float *x, float *y,
+                                  int warmup, int runs, double *samples) {
+  for (int i = 0; i < warmup; ++i) orc_omp_spmv_f32(m, rp, ci, val, x, y);
+  for (int i = 0; i < runs; ++i) {
+    double tic = omp_get_wtime();
+    orc_omp_spmv_f32(m, rp, ci, val, x, y);
+    samples[i] = omp_get_wtime() - tic;
+  }
+  return 0;
+}
+
+/* Thread placement for the CPU baseline (what OMP_PLACES + OMP_PROC_BIND=
+ * spread do, run_scripts/run_cuda_new.py:75-79; set here because libgomp
+ * reads those variables only once, at load, and binding the main thread at
+ * load shrinks the affinity mask bench.py reads).  Team thread t is bound to
+ * place t % n_places, place p being the CPUs cpus[off[p] .. off[p+1]).
+ * Returns the number of threads bound. */
+int orc_bind_threads(int nthreads, int n_places, const int *off, const int *cpus) {
+  int ok = 0;
+  if (nthreads < 1 || n_places < 1) return 0;
+  omp_set_num_threads(nthreads);
+#pragma omp parallel reduction(+ : ok)
+  {
+    const int p = omp_get_thread_num() % n_places;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (int i = off[p]; i < off[p + 1]; ++i) CPU_SET(cpus[i], &set);
+    ok += sched_setaffinity(0, sizeof(set), &set) == 0;
+  }
+  return ok;
+}
+
+/* First-touch copies of a CSR into caller-allocated, untouched buffers, in
+ * the static row partition omp_spmv's schedule(runtime) = static uses, so
+ * each thread's rows sit on its own NUMA node (spmv-csr/spmv.c reads the
+ * file on one thread; on a two-socket host that puts the whole matrix on
+ * one node and the timing on where the scheduler happened to run). */
+void orc_localize_csr(int64_t m, const int32_t *rp, const int32_t *ci, const void *val,
+                      int val_bytes, int32_t *rp2, int32_t *ci2, void *val2) {
+  int64_t row;
+#pragma omp parallel for schedule(static)
+  for (row = 0; row < m; ++row) {
+    const int32_t k0 = rp[row], k1 = rp[row + 1];
+    rp2[row] = k0;
+    memcpy(ci2 + k0, ci + k0, sizeof(int32_t) * (size_t)(k1 - k0));
+    memcpy((char *)val2 + (size_t)val_bytes * (size_t)k0, (const char *)val + (size_t)val_bytes * (size_t)k0,
+           (size_t)val_bytes * (size_t)(k1 - k0));
+  }
+  rp2[m] = rp[m];
 }
 
 int orc_max_threads(void) { return omp_get_max_threads(); }

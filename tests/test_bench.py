@@ -97,9 +97,12 @@ def test_bench_json_line_contract():
         assert plans[p]["y_bitwise_equal_to_headline"] is True
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
-    # the reported leg runs within the cgroup quota: TimeAvg close to TimeMin
+    # the reported leg leaves one CPU of the cgroup quota to the runtime
     if c["cgroup_cpu_quota"]:
-        assert c["cores"] <= c["cgroup_cpu_quota"]
+        assert c["cores"] <= c["cgroup_cpu_quota"] - 1 or c["cores"] == 1
+    assert c["time_min_s"] <= c["median_s"] <= c["time_max_s"]
+    assert c["threads_tried"][str(c["cores"])]["note"] == "reported leg"
+    assert d["strong_scaling"] is None  # N = 1: scaling_reference instead
     assert abs(c["value"] - 2 * d["config"]["nnz"] / c["time_min_s"] * 1e-9) < 1e-2 * c["value"]
     assert "nnz=51895117" in c["sample"]
     ref = c["reference_f32"]  # the reference's own omp_spmv, when oracle/_ref was built
@@ -109,7 +112,7 @@ def test_bench_json_line_contract():
     assert d["check"]["pass"] is True
     sr = d["scaling_reference"]  # C4 on this one GPU: the N = 1 point of the N > 1 curve
     assert sr["config"].startswith("c4") and sr["nnz"] > 199_999_000 and sr["value"] > 0
-    assert sr["check"]["pass"] is True
+    assert sr["check"]["pass"] is True and sr["cold_gflops"] > 0
 
 
 @pytest.mark.gpu
@@ -144,3 +147,9 @@ def test_bench_multi_rank_path_rehearsal_on_one_gpu(tmp_path):
     assert ov["chunks"] == 4 and ov["ms"] > 0 and ov["y_equal_to_plain_gather"] is True
     assert d["cpu_baseline"] is None              # rank 0 at N = 1 only
     assert d["scaling_reference"] is None
+    sc = d["strong_scaling"]  # the same workload on rank 0's GPU alone, same job
+    assert sc["n1"]["config"].startswith("c2") and sc["n1"]["n_gpus"] == 1
+    assert sc["n1"]["check"]["pass"] is True and sc["n1_gflops"] > 0
+    assert abs(sc["efficiency"] - d["value"] / (2 * sc["n1_gflops"])) < 1e-3
+    assert sc["cold_gflops"] > 0 and sc["n1_cold_gflops"] > 0
+    assert abs(sc["cold_efficiency"] - sc["cold_gflops"] / (2 * sc["n1_cold_gflops"])) < 1e-3

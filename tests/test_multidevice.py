@@ -105,3 +105,7 @@ def test_bench_nccl_two_ranks():
     c = d["comm"]
     assert c["bcast_x_ms"] > 0 and c["gather_y_ms"] > 0 and c["halo_x_ms"] > 0
     assert c["overlap"]["y_equal_to_plain_gather"] is True
+    sc = d["strong_scaling"]  # C4 whole on rank 0's GPU, same job
+    assert sc["n1"]["config"].startswith("c4") and sc["n1"]["check"]["pass"] is True
+    assert abs(sc["efficiency"] - d["value"] / (2 * sc["n1_gflops"])) < 1e-3
+    assert sc["cold_efficiency"] > 0
