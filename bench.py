@@ -47,9 +47,10 @@ Extra fields on the line:
                read as super-linear scaling
   cpu_baseline the oracle's OpenMP restatement of spmv-csr's omp_spmv on the
                host cores, on the SAME matrix (rank 0 at N = 1 only, bounded
-               sample), value from TimeMin as run_norm.py records it (median
-               and TimeAvg beside it), on the cgroup CPU quota minus one
-               thread, one per L3 domain, matrix first-touched per thread; beside it
+               sample, a process of its own: oracle/cpu_bench.py), value from
+               TimeMin as run_norm.py records it (median and TimeAvg beside
+               it), on the cgroup CPU quota minus one thread, one per L3
+               domain, matrix first-touched per thread; beside it
                reference_f32: the reference's own omp_spmv (spmv-csr/spmv.c,
                built unmodified into oracle/_ref) on the fp32 copy
 """
@@ -57,7 +58,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import re
 import subprocess
@@ -71,10 +71,6 @@ from pathlib import Path
 # baseline reads its thread count from to that core (r02x: 2 threads,
 # 11.5 GFLOP/s instead of 128 threads, 144 GFLOP/s).
 os.environ.setdefault("OMP_SCHEDULE", "static")
-# idle OpenMP workers sleep instead of spinning between the baseline's timed
-# runs: spinning workers compete with the Python / HIP runtime threads for the
-# cgroup CPU quota, and a throttled period shows up as a slow run
-os.environ.setdefault("OMP_WAIT_POLICY", "passive")
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "heterogeneous-spmv_amd"))
@@ -213,177 +209,39 @@ def load_traffic(workload_key: str):
 
 # ------------------------------------------------------------------ CPU baseline
 
-def host_cpu_info() -> dict:
-    """Physical cores from lscpu (Core(s) per socket x Socket(s)), the CPUs
-    this process may run on, and the cgroup CPU quota (cpu.max), if any."""
-    info = {"physical_cores": None, "affinity_cpus": len(os.sched_getaffinity(0)),
-            "cgroup_cpu_quota": None, "model": None}
-    try:
-        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
-        kv = {}
-        for line in out.splitlines():
-            k, _, v = line.partition(":")
-            kv[k.strip()] = v.strip()
-        cps, sock = int(kv.get("Core(s) per socket", "0")), int(kv.get("Socket(s)", "0"))
-        if cps and sock:
-            info["physical_cores"] = cps * sock
-        info["model"] = kv.get("Model name")
-    except Exception:
-        pass
-    try:
-        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
-        if q != "max":
-            info["cgroup_cpu_quota"] = float(q) / float(per)
-    except Exception:
-        pass
-    return info
-
-
-def l3_places(cpus) -> list:
-    """One place per L3 domain (an EPYC CCD) of the given CPUs, physical cores
-    only (the first SMT sibling of each core), ordered so that consecutive
-    places alternate between sockets: what OMP_PLACES=ll_caches +
-    OMP_PROC_BIND=spread give.  [] when sysfs lacks the cache topology."""
-    def rd(c, f):
-        return Path(f"/sys/devices/system/cpu/cpu{c}/{f}").read_text().strip()
-    dom = {}
-    try:
-        for c in sorted(cpus):
-            sib = rd(c, "topology/thread_siblings_list").replace("-", ",").split(",")
-            if int(sib[0]) != c and int(sib[0]) in cpus:
-                continue  # not the first hardware thread of its core
-            key = (int(rd(c, "topology/physical_package_id")), int(rd(c, "cache/index3/id")))
-            dom.setdefault(key, []).append(c)
-    except (OSError, ValueError):
-        return []
-    by_pkg = {}
-    for (pkg, l3), cs in sorted(dom.items()):
-        by_pkg.setdefault(pkg, []).append(cs)
-    out = []
-    for i in range(max(len(v) for v in by_pkg.values()) if by_pkg else 0):
-        for pkg in sorted(by_pkg):
-            if i < len(by_pkg[pkg]):
-                out.append(by_pkg[pkg][i])
-    return out
-
-
-def _timing(A, nnz, samples):
-    tmin, tmax = float(samples.min()), float(samples.max())
-    tavg, tmed = float(samples.mean()), float(np.median(samples))
-    g = lambda t: round(2.0 * nnz / t * 1e-9, 3)  # noqa: E731
-    return {"time_min_s": tmin, "time_avg_s": tavg, "time_max_s": tmax, "median_s": tmed,
-            "avg_over_min": round(tavg / tmin, 3), "gflops_from_min": g(tmin),
-            "gflops_from_median": g(tmed), "gflops_from_avg": g(tavg), "runs": int(samples.size)}
+# OpenMP wait policy of the CPU-baseline process (None: libgomp's default,
+# spin then sleep).  Measured on the GPU box (profiles/r04b_cpu_baseline_ab.jsonl).
+CPU_WAIT_POLICY = None
 
 
 def cpu_baseline(A, x, budget_s: float):
-    """The oracle's OpenMP restatement of omp_spmv (spmv-csr/spmv.c:92-114) on
-    the same matrix, timed with the reference protocol (5 warm-ups + N timed
-    runs, omp_get_wtime per run; spmv.c:164-185) on this host's cores.
-    value = 2 nnz / TimeMin (run_norm.py records min/max/avg; BASELINE.md §3);
-    the median and TimeAvg are reported beside it.
-
-    Threads: the reported leg runs one thread fewer than the cgroup CPU quota
-    (cpu.max) allows, so the Python / HIP runtime threads have a CPU of
-    headroom and the leg is never throttled (r03: 16 threads exactly filling a
-    16-CPU quota gave TimeAvg/TimeMin 1.35 on one box and 1.88 on another, a
-    baseline that moved 11 %); without a quota, the physical cores.  The
-    team is spread one thread per L3 domain (OMP_PROC_BIND=spread over
-    ll_caches places, run_cuda_new.py:75-79 binds too) and the matrix is
-    first-touch copied in the static row partition, so each thread streams
-    its rows from its own NUMA node.  The full-quota and all-core counts are
-    timed first, unbound, and listed in threads_tried as bursts, never
-    reported as value."""
-    sys.path.insert(0, str(REPO / "oracle"))
-    import oracle  # test infrastructure: the CPU baseline leg only
-    hw = host_cpu_info()
-    phys = hw["physical_cores"] or hw["affinity_cpus"]
-    avail = max(1, min(phys, hw["affinity_cpus"]))
-    quota = hw["cgroup_cpu_quota"]
-    threads = max(1, min(avail, int(math.floor(quota)) - 1)) if quota else avail
-    tried = {}
-    for t in sorted({min(avail, int(math.floor(quota))) if quota else avail, avail} - {threads}):
-        oracle.set_schedule("static", t)
-        tm = _timing(A, A.nnz, oracle.time_spmv_samples(A.row_ptr, A.col_idx, A.val, x, 5, 20))
-        tm["within_quota"] = bool(not quota or t <= quota)
-        tm["note"] = ("burst: above the cgroup CPU quota, throttled on average" if quota and t > quota
-                      else "no CPU left for the runtime threads: throttled in some periods")
-        tried[int(t)] = tm
-    oracle.set_schedule("static", threads)
-    places = l3_places(os.sched_getaffinity(0))
-    bound = oracle.bind_threads(threads, places) if places else 0
-    rp, ci, val = oracle.localize(A.row_ptr, A.col_idx, A.val)
-    per = max(float(np.median(oracle.time_spmv_samples(rp, ci, val, x, 2, 5))), 1e-6)
-    runs = int(max(20, min(20000, 0.4 * budget_s / per)))
-    res = {}
-    for sched in ("static", "guided"):  # run_norm.py:18,66 / run_cuda_new.py:79
-        oracle.set_schedule(sched, threads)
-        res[sched] = _timing(A, A.nnz, oracle.time_spmv_samples(rp, ci, val, x, 5, runs))
-    oracle.set_schedule("static", threads)
-    st = res["static"]
-    tried[int(threads)] = dict(st, within_quota=True, note="reported leg")
-    dt = "fp64" if A.val.dtype == np.float64 else "fp32"
-    placement = (f"one thread per L3 domain ({len(places)} domains, {bound} threads bound)"
-                 if bound else "unbound (no cache topology in sysfs)")
-    return {"value": st["gflops_from_min"], "unit": "GFLOP/s", "cores": int(threads),
-            "kind": "port",
-            "cores_note": ((f"{int(threads)} OpenMP threads = the cgroup quota of {quota} CPUs "
-                            f"minus one for the runtime threads" if quota else
-                            f"{int(threads)} OpenMP threads = the physical cores (no cgroup quota)")
-                           + f" ({phys} physical cores, {hw['affinity_cpus']} CPUs in the affinity "
-                           f"mask); {placement}, OMP_WAIT_POLICY={os.environ.get('OMP_WAIT_POLICY')}"),
-            "cgroup_cpu_quota": quota,
-            "sample": (f"the same matrix as the GPU line (m={A.m}, nnz={A.nnz}, {dt}, CSR), "
-                       f"omp_spmv restatement (oracle/spmv_oracle.c), OMP_SCHEDULE=static, "
-                       f"{int(threads)} threads, 5 warm-ups + {runs} timed runs "
-                       f"(spmv-csr/spmv.c:164-185 protocol), value = 2 nnz / TimeMin"),
-            "time_min_s": st["time_min_s"], "time_avg_s": st["time_avg_s"],
-            "time_max_s": st["time_max_s"], "median_s": st["median_s"],
-            "avg_over_min": st["avg_over_min"], "gflops_from_median": st["gflops_from_median"],
-            "gflops_from_avg": st["gflops_from_avg"],
-            "host": hw, "threads_tried": tried,
-            "guided": {"gflops": res["guided"]["gflops_from_min"],
-                       "gflops_from_median": res["guided"]["gflops_from_median"],
-                       "gflops_from_avg": res["guided"]["gflops_from_avg"],
-                       "time_min_s": res["guided"]["time_min_s"],
-                       "median_s": res["guided"]["median_s"], "runs": runs}}, threads
-
-
-def reference_cpu(A, x, threads: int, budget_s: float):
-    """The reference's own omp_spmv (spmv-csr/spmv.c:92-114, compiled
-    unmodified from /root/reference into oracle/_ref by oracle/Makefile) on
-    the fp32 copy of the same matrix (its only dtype), same protocol: 5
-    warm-ups + N timed calls.  None when the library was not built."""
-    sys.path.insert(0, str(REPO / "oracle"))
-    import ctypes as C
-    import oracle
-    if not oracle.ref_available():
-        return None
-    R = oracle.ref()
-    oracle.set_schedule("static", threads)  # the team bound by cpu_baseline
-    rp, ci, v = oracle.localize(A.row_ptr, A.col_idx, np.ascontiguousarray(A.val, np.float32))
-    xx = np.ascontiguousarray(x, np.float32)
-    y = np.zeros(A.m, np.float32)
-    args = (C.c_int(A.m), C.c_int(xx.shape[0]), C.c_int(A.nnz), rp.ctypes.data, ci.ctypes.data,
-            v.ctypes.data, xx.ctypes.data, y.ctypes.data)
-    for _ in range(5):
-        R.omp_spmv(*args)
-    ts = []
-    t_end = time.perf_counter() + budget_s
-    while len(ts) < 20 or (time.perf_counter() < t_end and len(ts) < 20000):
-        t0 = time.perf_counter()
-        R.omp_spmv(*args)
-        ts.append(time.perf_counter() - t0)
-    tm = _timing(A, A.nnz, np.array(ts))
-    return {"kind": "reference", "dtype": "f32", "cores": threads,
-            "value": tm["gflops_from_min"], "unit": "GFLOP/s",
-            "avg_over_min": tm["avg_over_min"], "gflops_from_avg": tm["gflops_from_avg"],
-            "gflops_from_median": tm["gflops_from_median"], "median_s": tm["median_s"],
-            "time_min_s": tm["time_min_s"], "time_avg_s": tm["time_avg_s"],
-            "time_max_s": tm["time_max_s"], "runs": tm["runs"],
-            "sample": (f"the reference's omp_spmv (oracle/_ref, built from spmv-csr/spmv.c) on the "
-                       f"same matrix in fp32, OMP_SCHEDULE=static, {threads} threads, 5 warm-ups + "
-                       f"{len(ts)} timed calls, value = 2 nnz / TimeMin")}
+    """The CPU legs (oracle/cpu_bench.py: the oracle's omp_spmv restatement,
+    spmv-csr/spmv.c:92-114, and the reference's own omp_spmv in fp32) on the
+    SAME matrix, in a process of their own: the matrix and x go through a
+    scratch directory, the legs' JSON comes back on stdout.  value = 2 nnz /
+    TimeMin (run_norm.py records min/max/avg), median and
+    TimeAvg beside it; threads = the cgroup CPU quota minus one, one per L3
+    domain, matrix first-touched per thread (see oracle/cpu_bench.py)."""
+    import shutil
+    import tempfile
+    d = Path(tempfile.mkdtemp(prefix="hspmv_cpu_", dir="/dev/shm" if Path("/dev/shm").is_dir() else None))
+    try:
+        np.save(d / "row_ptr.npy", np.ascontiguousarray(A.row_ptr, np.int32))
+        np.save(d / "col_idx.npy", np.ascontiguousarray(A.col_idx, np.int32))
+        np.save(d / "val.npy", np.ascontiguousarray(A.val))
+        np.save(d / "x.npy", np.ascontiguousarray(x, A.val.dtype))
+        env = {k: v for k, v in os.environ.items() if not k.startswith(("OMP_", "GOMP_"))}
+        env["OMP_SCHEDULE"] = "static"
+        if CPU_WAIT_POLICY:
+            env["OMP_WAIT_POLICY"] = CPU_WAIT_POLICY
+        out = subprocess.run([sys.executable, str(REPO / "oracle" / "cpu_bench.py"), "--dir", str(d),
+                              "--budget", str(budget_s)], env=env, capture_output=True, text=True,
+                             timeout=600)
+        if out.returncode != 0:
+            raise RuntimeError(f"oracle/cpu_bench.py failed: {out.stderr[-1500:]}")
+        return json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def single_gpu_point(args, stream, cfg: str):
@@ -714,8 +572,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, threads = cpu_baseline(A, x_host, args.cpu_seconds)
-        cpu["reference_f32"] = reference_cpu(A, x_host, threads, 0.5 * args.cpu_seconds)
+        cpu = cpu_baseline(A, x_host, args.cpu_seconds)
 
     if rank == 0:
         ctype = "double" if np_dt == np.float64 else "float"

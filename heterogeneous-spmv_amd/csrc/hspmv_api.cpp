@@ -424,7 +424,7 @@ static int fill_info(hspmv_handle *h, hspmv_info *out) {
   // sent it to the CSR3 kernel runs build_tasks' row groups
   out->csr3_plan = s.plan.kernel != kCsr3 ? 0
                    : s.A.n_ssr == 0 ? HSPMV_CSR3_PLAN_ROW_GROUPS
-                   : s.h_tasks.empty() ? HSPMV_CSR3_PLAN_SSR
+                   : s.tune.csr3_plan == HSPMV_CSR3_PLAN_SSR ? HSPMV_CSR3_PLAN_SSR
                    : csr3_fill(s.tune) ? HSPMV_CSR3_PLAN_ALIGNED : HSPMV_CSR3_PLAN_PACKED;
   out->csort_slot_bytes = s.plan.kernel == kCsort ? (s.dp.cs.slot32 ? 4 : 8) : 0;
   out->csort_row_blocks = s.plan.kernel == kCsort ? s.dp.cs.row_blocks : 0;
@@ -461,6 +461,17 @@ int hspmv_diag_csort_trace(hspmv_handle *h, unsigned long long *out, int max_wg)
   if (hipSetDevice(s.device) != hipSuccess || hipStreamSynchronize(s.stream) != hipSuccess ||
       hipMemcpy(out, s.dp.cs.trace, 24 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
     return 0;
+  return n;
+}
+
+// Diagnostic builds only: build_csort's per-workgroup cost terms {rows,
+// slices, chunks, entries, gather quad-sectors, gather sectors, segmented
+// chunks, 0} (8 int64 per workgroup).  Returns the workgroup count.
+int hspmv_diag_csort_stats(hspmv_handle *h, long long *out, int max_wg) {
+  if (!h || h->shards.empty()) return 0;
+  const Shard &s = h->shards[0];
+  const int n = std::min<int>(max_wg, (int)(s.csort_wg_stats.size() / 8));
+  memcpy(out, s.csort_wg_stats.data(), 8 * 8 * (size_t)n);
   return n;
 }
 #endif

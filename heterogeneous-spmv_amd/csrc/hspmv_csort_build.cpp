@@ -260,6 +260,13 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     val64.assign((size_t)tot, 0.0);
   }
   std::atomic<int64_t> n_seg{0};  // chunks stored slot-sorted (segmented)
+  // diagnostic builds (Tuning.csort_trace): per workgroup {rows, slices,
+  // chunks, entries, gather quad-sectors, gather sectors, segmented chunks,
+  // 0} -- the cost terms the per-workgroup timelines are compared with
+  constexpr int kWgStats = 8;
+  const bool stats = tn.csort_trace == 1;
+  std::vector<int64_t> wst(stats ? (size_t)(kWgStats * G) : 0, 0);
+  const int sec_shift = dtype == HSPMV_F32 ? 3 : 2;  // x entries per 32-byte sector: 8 / 4
   {
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t)
@@ -332,6 +339,28 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
               }
             }
             cbase[(size_t)ch] = (int32_t)(c0 | (seg ? 0x80000000u : 0u));
+            if (stats) {
+              int64_t *w = wst.data() + kWgStats * b;
+              w[2] += 1;
+              w[3] += j - i;
+              w[6] += seg ? 1 : 0;
+              for (int64_t g = 0; g < C; g += 64) {  // one gather instruction
+                uint32_t sec[64];
+                for (int64_t q = 0; q < 64; ++q)
+                  sec[q] = (i + g + q < j ? src[g + q].col : c0) >> sec_shift;
+                for (int64_t q = 0; q < 64; q += 4) {  // the L1 serves each quad on its own
+                  int d = 1;
+                  for (int t = 1; t < 4; ++t) {
+                    bool seen = false;
+                    for (int t2 = 0; t2 < t; ++t2) seen |= sec[q + t] == sec[q + t2];
+                    d += seen ? 0 : 1;
+                  }
+                  w[4] += d;
+                }
+                std::sort(sec, sec + 64);
+                w[5] += (int64_t)(std::unique(sec, sec + 64) - sec);
+              }
+            }
             for (int64_t q = 0; q < C; ++q) {
               const int64_t o = ch * C + at(q, dtype == HSPMV_F32 ? 2 : 4);
               const int64_t ov = ch * C + at(q, 2);
@@ -419,6 +448,13 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.blk_v = s.d_cs_blk_v;
   c.row_blocks = (int32_t)NB;
   s.csort_seg_chunks = n_seg.load();
+  if (stats) {
+    for (int64_t b = 0; b < G; ++b) {
+      wst[(size_t)(kWgStats * b)] = wg_rows[(size_t)(2 * b + 1)] - wg_rows[(size_t)(2 * b)];
+      wst[(size_t)(kWgStats * b + 1)] = (int64_t)wg_sl[(size_t)b].size();
+    }
+    s.csort_wg_stats.swap(wst);
+  }
   s.csort_chunks = tot_chunks;
   if (tn.csort_trace == 1 && (rc = dev_alloc(&s.d_cs_trace, 24 * (size_t)G, &s.bytes))) return rc;
   c.trace = s.d_cs_trace;

@@ -32,7 +32,8 @@ struct DevCSR {
   bool has_xwin = false, has_xdict = false;
   bool has_xdict_tasks = false;  // x dictionaries built for packed CSR3 tasks
   int32_t n_slabs = 1;        // x slabs: the row kernel's passes (each sees ~nnz / n_slabs)
-  int32_t task_waves = 4;     // CSR3 packed tasks per workgroup (4, or 8 with x dictionaries)
+  int32_t task_waves = 4;     // CSR3 wave tasks per workgroup: 4 (8 with 8-task dictionary
+                              // blocks); the SSR plan: ssr_waves() per super-super-row
   bool has_csort = false;     // column-sorted row blocks were built (irregular gathers)
 };
 
@@ -165,6 +166,13 @@ struct LaunchPlan {
   int32_t carry = 0;       // STREAM/CSR3: rows start from y (x-slab passes after the first)
   int64_t blocks = 0;
 };
+
+// Waves of the workgroup-per-super-super-row CSR-3 plan: ~64 rows per wave
+// (one lane per row in the ordered sums), from the mean rows per SSR.
+inline int ssr_waves(double rows_per_ssr) {
+  const double w = rows_per_ssr / 64.0;
+  return w >= 6.0 ? 8 : (w >= 3.0 ? 4 : (w >= 1.5 ? 2 : 1));
+}
 
 // Chooses kernel / lanes / block shape for a shard (host-side heuristic).
 // rows_per_ssr: mean rows per super-super-row (CSR-3 workgroup-per-SSR plan);

@@ -73,6 +73,7 @@ struct Shard {
   DevCsort csort;
   double csort_format_bytes = 0.0;   // bytes one csort SpMV moves
   int64_t csort_chunks = 0, csort_seg_chunks = 0;  // chunks, and those stored slot-sorted
+  std::vector<int64_t> csort_wg_stats;  // diagnostic builds: 8 cost terms per workgroup
   int c16g_shape = 0;                // group-base columns built for kStream groups / kCsr3 tasks
   std::vector<int32_t> h_xwin;       // built at upload (host columns at hand)
   std::vector<int32_t> h_xwin_t;     // the same per packed CSR-3 task
@@ -155,8 +156,9 @@ int place_shard(Shard &s, int64_t n, int dtype);
 int64_t count_distinct_cols(const int32_t *col, int64_t nnz, int64_t n);
 bool csr3_packed(const Tuning &t);
 bool csr3_fill(const Tuning &t);
-void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner, unsigned flags,
-                 const Tuning &tune, std::vector<int32_t> &ts);
+void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner,
+                 const std::vector<int32_t> *outer, unsigned flags, const Tuning &tune,
+                 std::vector<int32_t> &ts, int *waves);
 bool irregular_gathers(const int32_t *rp, const int32_t *col, int64_t m, double sv);
 int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
                      int64_t n, int dtype, unsigned flags);

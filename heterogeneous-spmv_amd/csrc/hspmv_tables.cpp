@@ -197,8 +197,43 @@ int build_col16g(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int
 // super-super-row spans as many waves as its rows need instead of a fixed W
 // per launch (handCoarsen's super-super-rows vary ~10x in rows).
 // Tuning.csr3_plan = HSPMV_CSR3_PLAN_SSR selects the workgroup-per-super-
-// super-row plan.
+// super-row plan (ssr_tasks).
 bool csr3_packed(const Tuning &t) { return t.csr3_plan != HSPMV_CSR3_PLAN_SSR; }
+
+// The workgroup-per-super-super-row plan (the reference's cuSpMV_3 mapping,
+// csrk.cu:245-319): W = ssr_waves(mean rows per SSR) tasks per SSR, each
+// SSR's super-rows split W ways by nonzeros -- wave w starts at the first
+// super-row reaching w/W of the SSR's nonzeros, but strictly after wave
+// w-1's start while super-rows remain: two waves never share a start (an
+// empty task beside a doubled one was 15 % of the tasks on a 64-row
+// grouping: 144 -> 129 us there).  Row-granular cuts capped at 64 rows per
+// wave measured 7-30 % slower on C3's groupings (long tails where an SSR
+// exceeds W*64 rows); profiles/r01_ab_csr3_tasks.jsonl.  Built with the
+// other host tables (not at plan time) so the block x dictionaries of the
+// packed plans apply to it: block b = SSR b.
+void ssr_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> &o,
+               const std::vector<int32_t> &in, int W, std::vector<int32_t> &ts) {
+  const int64_t nssr = (int64_t)o.size() - 1;
+  ts.assign((size_t)(nssr * W + 1), 0);
+  for (int64_t b = 0; b < nssr; ++b) {
+    const int32_t s0 = o[(size_t)b], s1 = o[(size_t)b + 1];
+    const int64_t k0 = rp[in[(size_t)s0]], k1 = rp[in[(size_t)s1]];
+    int32_t sr = s0, prev = s0 - 1;
+    for (int w = 0; w < W; ++w) {
+      const int64_t target = k0 + (k1 - k0) * w / W;
+      while (sr < s1 && rp[in[(size_t)sr]] < target) ++sr;
+      int32_t st = w == 0 ? s0 : sr;
+      if (st <= prev) st = prev + 1;
+      const int32_t latest = s1 - (W - w);  // leave one super-row per later wave
+      if (st > latest) st = std::max(prev + 1, latest);
+      if (st > s1) st = s1;
+      ts[(size_t)(b * W + w)] = in[(size_t)st];
+      prev = st;
+      sr = std::max(sr, st);
+    }
+  }
+  ts[(size_t)(nssr * W)] = (int32_t)m;
+}
 
 // Task cut of the packed CSR-3 plan: 64-row groups aligned to multiples of 64
 // rows (default), or whole super-rows packed up to 64 rows
@@ -268,16 +303,24 @@ void cap_task_nnz(const int32_t *rp, int32_t long_t, int32_t budget, std::vector
   ts.swap(out);
 }
 
-// The wave tasks of a shard (empty: STREAM's fixed 64-row groups, or the
-// workgroup-per-super-super-row CSR-3 plan).  CSR-3: the packed super-rows.
+// The wave tasks of a shard (empty: STREAM's fixed 64-row groups) and the
+// tasks per workgroup (*waves).  CSR-3: 64-row aligned groups or packed
+// super-rows, 4 per workgroup; or the SSR plan's W per super-super-row.
 // CSR under the auto (or CSR3) kernel: when at least a quarter of the
 // in-kernel nonzeros sit in 64-row groups over the budget, the 64-row groups
 // with the heavy ones cut -- the CSR3 kernel then runs them (a CSR-2 with
-// one-row super-rows).  Both are capped at the budget.
-void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner, unsigned flags,
-                 const Tuning &tune, std::vector<int32_t> &ts) {
+// one-row super-rows).  All but the SSR tasks are capped at the budget.
+void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner,
+                 const std::vector<int32_t> *outer, unsigned flags, const Tuning &tune,
+                 std::vector<int32_t> &ts, int *waves) {
   ts.clear();
-  if (!csr3_packed(tune)) return;
+  *waves = 4;
+  if (!csr3_packed(tune)) {
+    if (!inner || !outer || outer->size() < 2) return;
+    *waves = ssr_waves((double)m / (double)(outer->size() - 1));
+    ssr_tasks(rp, m, *outer, *inner, *waves, ts);
+    return;
+  }
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
   const int32_t budget = task_nnz_budget(tune);
   if (inner && csr3_fill(tune)) {
@@ -484,7 +527,10 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
 // kernels.
 int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
                      int64_t n, int dtype, unsigned flags) {
-  build_tasks(rp, m, s.A.n_ssr > 0 ? &s.h_inner : nullptr, flags, s.tune, s.h_tasks);
+  int waves = 4;
+  build_tasks(rp, m, s.A.n_ssr > 0 ? &s.h_inner : nullptr, s.A.n_ssr > 0 ? &s.h_outer : nullptr,
+              flags, s.tune, s.h_tasks, &waves);
+  s.A.task_waves = waves;
   s.h_xwin.clear();
   s.h_xwin_t.clear();
   int rc;
@@ -535,12 +581,9 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
   return HSPMV_OK;
 }
 
-// Host planner tables for one shard (needs s.h_rp, and s.h_outer/h_inner for
-// CSR-3):
-//  * split rows: rows longer than kLongRow, cut into kLongChunk pieces;
-//  * CSR-3 wave tasks: each super-super-row's super-rows split into
-//    waves_per_block contiguous ranges with ~equal nonzeros -- the first
-//    super-row s with rp[inner[s]] >= k0 + (k1-k0)*w/W starts wave w.
+// Host planner tables for one shard (needs s.h_rp): split rows (rows longer
+// than kLongRow, cut into kLongChunk pieces), and the device copies of the
+// tables build_row_tables planned (wave tasks, x windows).
 int build_plan_tables(Shard &s, int dtype, unsigned flags) {
   const std::vector<int32_t> &rp = s.h_rp;
   const int64_t m = s.A.m;
@@ -645,41 +688,6 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     HIP_TRY(hipMemcpy(s.d_task, s.h_tasks.data(), 4 * s.h_tasks.size(), hipMemcpyHostToDevice));
     s.dp.task_start = s.d_task;
     s.dp.n_tasks = (int32_t)(s.h_tasks.size() - 1);
-  } else if (s.plan.kernel == kCsr3) {
-    const std::vector<int32_t> &o = s.h_outer, &in = s.h_inner;
-    const int64_t nssr = s.A.n_ssr;
-    const int W = s.plan.waves_per_block;
-    std::vector<int32_t> ts((size_t)(nssr * W + 1));
-    for (int64_t b = 0; b < nssr; ++b) {
-      const int32_t s0 = o[b], s1 = o[b + 1];
-      const int64_t k0 = rp[in[s0]], k1 = rp[in[s1]];
-      // wave w starts at the first super-row reaching w/W of the nonzeros,
-      // but strictly after wave w-1's start while super-rows remain: two
-      // waves never share a start (an empty task beside a doubled one was
-      // 15 % of the tasks on a 64-row grouping: 144 -> 129 us there).
-      // Row-granular cuts capped at 64 rows per wave measured 7-30 % slower
-      // on C3's groupings (long tails where an SSR exceeds W*64 rows);
-      // profiles/r01_ab_csr3_tasks.jsonl.
-      int32_t sr = s0, prev = s0 - 1;
-      for (int w = 0; w < W; ++w) {
-        const int64_t target = k0 + (k1 - k0) * w / W;
-        while (sr < s1 && rp[in[sr]] < target) ++sr;
-        int32_t st = w == 0 ? s0 : sr;
-        if (st <= prev) st = prev + 1;
-        const int32_t latest = s1 - (W - w);  // leave one super-row per later wave
-        if (st > latest) st = std::max(prev + 1, latest);
-        if (st > s1) st = s1;
-        ts[(size_t)(b * W + w)] = in[st];
-        prev = st;
-        sr = std::max(sr, st);
-      }
-    }
-    ts[(size_t)(nssr * W)] = (int32_t)m;
-    int rc;
-    if ((rc = dev_alloc(&s.d_task, 4 * ts.size(), &s.bytes))) return rc;
-    HIP_TRY(hipMemcpy(s.d_task, ts.data(), 4 * ts.size(), hipMemcpyHostToDevice));
-    s.dp.task_start = s.d_task;
-    s.dp.n_tasks = (int32_t)(nssr * W);
   }
   return HSPMV_OK;
 }

@@ -38,7 +38,7 @@ int kernel_for_tables(int64_t n_ssr, bool have_tasks, unsigned flags) {
   const unsigned k = flags & 0xFu;
   if (k == kVector) return kVector;
   if ((k == kCsr3 || k == kAuto) && n_ssr > 0)
-    return have_tasks ? kCsr3 : -1;  // workgroup-per-SSR plan: no dictionaries
+    return have_tasks ? kCsr3 : -1;
   if ((k == kCsr3 || k == kAuto) && have_tasks) return kCsr3;  // CSR with heavy groups
   return kStream;
 }
@@ -150,15 +150,20 @@ bool plan_xdict(const int32_t *rp, const int32_t *col, const std::vector<int32_t
 // the barriers, twice the LDS per block).
 int xd_task_waves(const Tuning &t) { return t.xd_waves == 8 ? 8 : 4; }
 
-std::vector<int32_t> xdict_blocks(int kern, int64_t m, const std::vector<int32_t> &tasks,
-                                  const Tuning &tune) {
+// Tasks per dictionary block of a CSR3 task table: the SSR plan's W tasks
+// per super-super-row (one workgroup each), else xd_task_waves.
+int xd_block_tasks(const Tuning &t, int task_waves) {
+  return t.csr3_plan == HSPMV_CSR3_PLAN_SSR ? task_waves : xd_task_waves(t);
+}
+
+std::vector<int32_t> xdict_blocks(int kern, int64_t m, const std::vector<int32_t> &tasks, int W) {
   std::vector<int32_t> bs;
   if (kern == kStream) {
     for (int64_t r = 0; r < m; r += 256) bs.push_back((int32_t)r);
     bs.push_back((int32_t)m);
   } else {
     const int64_t nt = (int64_t)tasks.size() - 1;
-    for (int64_t t = 0; t < nt; t += xd_task_waves(tune)) bs.push_back(tasks[(size_t)t]);
+    for (int64_t t = 0; t < nt; t += W) bs.push_back(tasks[(size_t)t]);
     bs.push_back(tasks[(size_t)nt]);
   }
   return bs;
@@ -224,17 +229,19 @@ int64_t split_xd_blocks(std::vector<int32_t> &tasks, const std::vector<int32_t> 
 
 // plan_xdict over the workgroups of `kern`; CSR3 task tables are first cut
 // for occupancy (split_xd_blocks), so the plan is the one the kernel runs.
+// (The SSR plan's blocks are its super-super-rows: never cut.)
 bool plan_xdict_for(const int32_t *rp, const int32_t *col, int kern, int64_t m,
-                    std::vector<int32_t> &tasks, int32_t long_t, int64_t cap, int dtype,
+                    std::vector<int32_t> &tasks, int W, int32_t long_t, int64_t cap, int dtype,
                     const Tuning &tune, bool fill, XdPlan &P, int64_t *cut) {
   *cut = 0;
-  const bool cuts = kern == kCsr3 && xd_task_waves(tune) == 4 && tune.xd_blocks_per_cu >= 0;
-  if (!plan_xdict(rp, col, xdict_blocks(kern, m, tasks, tune), long_t, cap, fill && !cuts, P))
+  const bool cuts = kern == kCsr3 && W == 4 && tune.csr3_plan != HSPMV_CSR3_PLAN_SSR &&
+                    tune.xd_blocks_per_cu >= 0;
+  if (!plan_xdict(rp, col, xdict_blocks(kern, m, tasks, W), long_t, cap, fill && !cuts, P))
     return false;
   if (!cuts) return true;
   *cut = split_xd_blocks(tasks, P.total, xd_target_entries(dtype, tune));
   if (*cut == 0 && !fill) return true;
-  return plan_xdict(rp, col, xdict_blocks(kern, m, tasks, tune), long_t, cap, fill, P);
+  return plan_xdict(rp, col, xdict_blocks(kern, m, tasks, W), long_t, cap, fill, P);
 }
 
 // Auto mode also leaves banded matrices to the x windows (have_xwin: the
@@ -249,6 +256,8 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
   if (mode < 0 && have_xwin) return HSPMV_OK;
   const int kern = kernel_for_tables(s.A.n_ssr, !s.h_tasks.empty(), flags);
   if (kern != kStream && kern != kCsr3) return HSPMV_OK;
+  const int W = xd_block_tasks(s.tune, s.A.task_waves);
+  if (kern == kCsr3 && W != 4 && W != 8) return HSPMV_OK;  // the XD kernels run 4 or 8 waves
   if (kern == kStream && ((flags >> 29) & 0x7u) > 1) return HSPMV_OK;  // groups != 1
   const double sv = (double)dtype_size(dtype);
   const int64_t nnz = rp[m];
@@ -258,7 +267,7 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
   XdPlan P;
   // (cuts the task table only when the dictionaries are taken)
   std::vector<int32_t> tasks = s.h_tasks;
-  if (!plan_xdict_for(rp, col, kern, m, tasks, long_t, xdict_cap_entries(dtype, s.tune), dtype,
+  if (!plan_xdict_for(rp, col, kern, m, tasks, W, long_t, xdict_cap_entries(dtype, s.tune), dtype,
                       s.tune, true, P, &s.xd_cut))
     return HSPMV_OK;
   if (mode < 0 && 2 * P.entries > P.in_kernel_nnz) return HSPMV_OK;  // too little reuse to pay
@@ -275,7 +284,7 @@ int build_xdict(Shard &s, const int32_t *rp, const int32_t *col, int64_t m, int6
   s.A.cplanes = nullptr;
   s.A.n_cplanes = 0;
   s.xd_shape = kern;
-  if (kern == kCsr3) s.A.task_waves = xd_task_waves(s.tune);
+  if (kern == kCsr3) s.A.task_waves = W;
   s.xd_lds_bytes = (int32_t)((int64_t)P.tmax * (int64_t)sv);
   s.xd_entries = P.entries;
   s.xd_runs_n = (int64_t)P.rec.size() / 2;
@@ -303,20 +312,24 @@ int hspmv_xdict_plan_ex(const hspmv_csr *A, const hspmv_csr3_maps *maps, const h
   if ((rc = validate_host_maps(maps, A->m))) return rc;
   std::vector<int32_t> tasks;
   const bool csr3 = maps && maps->n_ssr > 0;
+  int waves = 4;
   if (csr3) {
     const std::vector<int32_t> inner(maps->inner, maps->inner + maps->n_sr + 1);
-    build_tasks(A->row_ptr, A->m, &inner, flags, tune, tasks);
+    const std::vector<int32_t> outer(maps->outer, maps->outer + maps->n_ssr + 1);
+    build_tasks(A->row_ptr, A->m, &inner, &outer, flags, tune, tasks, &waves);
   } else {
-    build_tasks(A->row_ptr, A->m, nullptr, flags, tune, tasks);
+    build_tasks(A->row_ptr, A->m, nullptr, nullptr, flags, tune, tasks, &waves);
   }
+  const int W = xd_block_tasks(tune, waves);
   const int kern = kernel_for_tables(csr3 ? maps->n_ssr : 0, !tasks.empty(), flags);
-  if ((kern != kStream && kern != kCsr3) || A->m == 0) return HSPMV_OK;
+  if ((kern != kStream && kern != kCsr3) || A->m == 0 || (kern == kCsr3 && W != 4 && W != 8))
+    return HSPMV_OK;
   if (cap_entries <= 0) cap_entries = xdict_cap_entries(A->dtype, tune);
   XdPlan P;
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
   const bool fill = blk || runs || pos;
   int64_t cut = 0;
-  if (!plan_xdict_for(A->row_ptr, A->col_idx, kern, A->m, tasks, long_t,
+  if (!plan_xdict_for(A->row_ptr, A->col_idx, kern, A->m, tasks, W, long_t,
                       std::min<int64_t>(cap_entries, 65536), A->dtype, tune, fill, P, &cut))
     return HSPMV_OK;  // some block exceeds the cap: no dictionary (n_blocks = 0)
   *n_blocks = (int64_t)P.blk.size() - 1;

@@ -792,8 +792,8 @@ hipError_t launch_rows(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, 
     return launch_rows_c<T, 0, true>(A, dp, p, x, y, st);
   }
   if (A.col16 && A.c16_mode == 2) {
-    if (p.kernel == kCsr3 && (!dp.task_start || p.waves_per_block != 4))
-      return hipErrorInvalidValue;  // built for the packed tasks, 4 per workgroup
+    if (p.kernel == kCsr3 && !dp.task_start)
+      return hipErrorInvalidValue;  // built for the host-planned wave tasks (one base per task)
     return launch_rows_c<T, 2, false>(A, dp, p, x, y, st);
   }
   return A.col16 ? launch_rows_c<T, 1, false>(A, dp, p, x, y, st)

@@ -317,8 +317,8 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
     }
     case kCsr3: {
       p.lanes = kWave;
-      if (packed_tasks > 0) {  // super-rows packed into <= 64-row tasks, 4 (or 8) per block
-        p.waves_per_block = A.task_waves == 8 ? 8 : 4;
+      if (packed_tasks > 0) {  // host-planned wave tasks: task_waves per block
+        p.waves_per_block = (A.task_waves == 1 || A.task_waves == 2 || A.task_waves == 8) ? A.task_waves : 4;
         const double rows_per_task = (double)A.m / (double)packed_tasks;
         const double per_pass = (rows_per_task < 64.0 ? rows_per_task : 64.0) * d;
         p.u = forced_u ? forced_u : pick_u(per_pass < 64.0 * kLongRow ? per_pass : 64.0 * kLongRow, dtype, A.n_slabs > 1);
@@ -326,8 +326,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
         break;
       }
       // ~64 rows per wave (one lane per row in the ordered sums)
-      const double w = rows_per_ssr / 64.0;
-      p.waves_per_block = w >= 6.0 ? 8 : (w >= 3.0 ? 4 : (w >= 1.5 ? 2 : 1));
+      p.waves_per_block = ssr_waves(rows_per_ssr);
       const double rows_per_task = rows_per_ssr / p.waves_per_block;
       const double per_pass = (rows_per_task < 64.0 ? rows_per_task : 64.0) * d;
       p.u = forced_u ? forced_u : pick_u(per_pass < 64.0 * kLongRow ? per_pass : 64.0 * kLongRow, dtype, A.n_slabs > 1);

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""A/B of the CPU baseline's process settings on the bench's C3 matrix
+(oracle/cpu_bench.py in a process of its own per variant): OpenMP wait
+policy (libgomp default / passive / active) x thread placement (one per L3
+domain / unbound), each variant twice, interleaved.  One JSON line per run.
+
+    python heterogeneous-spmv_amd/tools/cpu_baseline_ab.py --out F.jsonl [--budget 6]
+"""
+import argparse
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parents[1]
+sys.path.insert(0, str(HERE.parent))
+from hspmv import dist as hdist  # noqa: E402
+from hspmv import gen  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--budget", type=float, default=6.0)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    sh = hdist.build_shard(a.config, 0, 1)
+    A = sh.A
+    d = Path(tempfile.mkdtemp(prefix="hspmv_cpuab_", dir="/dev/shm"))
+    np.save(d / "row_ptr.npy", A.row_ptr)
+    np.save(d / "col_idx.npy", A.col_idx)
+    np.save(d / "val.npy", A.val)
+    np.save(d / "x.npy", gen.rand_x(A.n, 42, dtype=A.val.dtype))
+    variants = [(pol, bind) for pol in (None, "passive", "active") for bind in (True, False)]
+    with open(a.out, "w") as f:
+        for rep in range(a.reps):
+            for pol, bind in variants:
+                env = {k: v for k, v in os.environ.items() if not k.startswith(("OMP_", "GOMP_"))}
+                env["OMP_SCHEDULE"] = "static"
+                if pol:
+                    env["OMP_WAIT_POLICY"] = pol
+                cmd = [sys.executable, str(REPO / "oracle" / "cpu_bench.py"), "--dir", str(d),
+                       "--budget", str(a.budget), "--no-tried"] + ([] if bind else ["--no-bind"])
+                out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+                r = json.loads(out.stdout.strip().splitlines()[-1]) if out.returncode == 0 else {}
+                rec = {"config": a.config, "rep": rep, "wait_policy": pol or "default", "bind": bind,
+                       "rc": out.returncode, "err": out.stderr[-300:] if out.returncode else ""}
+                for k in ("value", "gflops_from_median", "gflops_from_avg", "avg_over_min", "cores"):
+                    rec[k] = r.get(k)
+                ref = r.get("reference_f32") or {}
+                rec["ref_value"], rec["ref_avg_over_min"] = ref.get("value"), ref.get("avg_over_min")
+                print(json.dumps(rec), flush=True)
+                f.write(json.dumps(rec) + "\n")
+    shutil.rmtree(d, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

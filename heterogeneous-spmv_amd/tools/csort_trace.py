@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--lib", default=str(HERE.parent / "build" / "diagenv" / "libhspmv.so"))
     ap.add_argument("--env", default="", help="extra A/B knobs K=V,K=V for the handle")
     ap.add_argument("--out", default="")
+    ap.add_argument("--per-wg", action="store_true", help="every workgroup + the build's cost terms")
     a = ap.parse_args()
     L = load(a.lib)
     L.hspmv_diag_csort_trace.restype = C.c_int
@@ -72,7 +73,34 @@ def main():
                                       for i in range(8)],
                "slowest": [{"wg": int(j), "part": int(j % 2), "xcc": int(xcc[j]),
                             "start": round(float(st[j]), 2), "dur": round(float(dur[j]), 2)} for j in slow]}
-        print(json.dumps(rec), flush=True)
+        if a.per_wg:  # every workgroup, with build_csort's cost terms beside it
+            L.hspmv_diag_csort_stats.restype = C.c_int
+            L.hspmv_diag_csort_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+            stt = np.zeros((4096, 8), np.int64)
+            ns = L.hspmv_diag_csort_stats(h, stt.ctypes.data, 4096)
+            names = ["rows", "slices", "chunks", "entries", "quad_sectors", "sectors", "seg_chunks"]
+            rec["per_wg"] = {"start_us": np.round(st, 2).tolist(), "dur_us": np.round(dur, 2).tolist(),
+                             "xcc": xcc.tolist()}
+            if ns == n:
+                for i, nm in enumerate(names):
+                    rec["per_wg"][nm] = stt[:n, i].tolist()
+                # least squares: duration against the cost terms (+ constant)
+                X = np.column_stack([stt[:n, 3], stt[:n, 4], stt[:n, 0], stt[:n, 6], np.ones(n)]).astype(float)
+                coef, *_ = np.linalg.lstsq(X, dur, rcond=None)
+                pred = X @ coef
+                rec["fit"] = {"terms": ["entries", "quad_sectors", "rows", "seg_chunks", "const"],
+                              "coef_us": [float(c) for c in coef],
+                              "r2": float(1 - np.sum((dur - pred) ** 2) / np.sum((dur - dur.mean()) ** 2)),
+                              "corr": {nm: float(np.corrcoef(stt[:n, i], dur)[0, 1]) for i, nm in enumerate(names)
+                                       if np.std(stt[:n, i]) > 0}}
+                for part in range(int(stt[:n, 0].size and 2)):
+                    sel = np.arange(n) % 2 == part
+                    rec.setdefault("by_part", []).append(
+                        {"part": part, "dur_median": float(np.median(dur[sel])), "dur_max": float(dur[sel].max()),
+                         "entries_median": float(np.median(stt[:n, 3][sel])),
+                         "quad_sectors_median": float(np.median(stt[:n, 4][sel])),
+                         "rows_median": float(np.median(stt[:n, 0][sel]))})
+        print(json.dumps({k: v for k, v in rec.items() if k != "per_wg"}), flush=True)
         out.append(rec)
         L.hspmv_destroy(h)
     if a.out:

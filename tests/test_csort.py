@@ -196,10 +196,17 @@ def test_csort_segmented_chunks_for_contiguous_hub_rows(dtype):
         # scan ran), and only those: most chunks stay in column order
         assert 0 < info["csort_seg_chunks"] < info["csort_chunks"] // 2, info
         check(A, x, y)
-    # random columns: no instruction crowds one slot, no segmented chunk
-    B = gen.powerlaw(60_000, seed=5, dtype=dtype)
+    # short rows over random columns: no instruction crowds one slot, so no
+    # chunk is segmented (power-law hubs with thousands of random columns
+    # can crowd one: those chunks are segmented by the same rule)
+    rng = np.random.default_rng(7)
+    lens = rng.integers(0, 30, 40_000)
+    rp = np.concatenate([[0], np.cumsum(lens)])
+    ci = np.concatenate([np.sort(rng.choice(400_000, ln, replace=False)) for ln in lens])
+    B = hspmv.CsrMatrix(40_000, 400_000, rp, ci, rng.uniform(-1, 1, rp[-1]).astype(dtype))
     y, info = run(B, gen.rand_x(B.n, 3).astype(dtype), kernel="csort")
     assert info["csort_chunks"] > 0 and info["csort_seg_chunks"] == 0
+    check(B, gen.rand_x(B.n, 3).astype(dtype), y)
 
 
 def test_csort_rcm_powerlaw_matches_oracle():

@@ -128,6 +128,30 @@ def test_csr3_map_sizes(waves_case, plan):
         check_fp64(A, x, y, exact_rows=short_rows(A))
 
 
+@pytest.mark.parametrize("waves_case", [(20, 10), (7, 8), (64, 4), (400, 2)])
+def test_csr3_ssr_plan_with_x_dictionaries(waves_case):
+    """The workgroup-per-super-super-row plan (the reference's cuSpMV_3
+    mapping) stages a block x dictionary per super-super-row when its W
+    waves are 4 or 8 -- one workgroup, one SSR, one dictionary -- and its y
+    is bit for bit the aligned plan's (row sums are row-local)."""
+    ssrs, srs = waves_case
+    A = gen.stencil27(40)
+    maps = hspmv.build_csr3_maps(A, ssrs, srs)
+    x = gen.rand_x(A.n, 9)
+    y0, i0 = gpu_spmv(A, x, maps, options={"csr3_plan": "aligned", "x_dict": -1})
+    y1, i1 = gpu_spmv(A, x, maps, options={"csr3_plan": "ssr", "x_dict": 1})
+    assert i1["csr3_plan"] == 3 and i1["wave_tasks"] == maps.n_ssr * i1["waves_per_block"]
+    assert i1["blocks"] == maps.n_ssr
+    # the host planner's view (hspmv_xdict_plan_ex): W of 4 or 8 and every
+    # SSR's dictionary within the LDS cap
+    planned = hspmv.xdict_plan(A, maps, kernel="csr3", options={"csr3_plan": "ssr", "x_dict": 1})
+    assert i1["x_dict"] == (1 if planned is not None else 0), i1
+    if planned is not None:
+        assert planned[0].size - 1 == maps.n_ssr and i1["waves_per_block"] in (4, 8)
+    assert np.array_equal(y0, y1)
+    check_fp64(A, x, y1, exact_rows=short_rows(A))
+
+
 @pytest.mark.parametrize("xwin", ["0", "1"])
 def test_x_window_variants_identical(xwin):
     """Global gathers and LDS x windows give the same bits (the windows only
