@@ -35,6 +35,12 @@ constexpr int32_t kCsortSlice = 2048;
 // lanes in all is stored slot-sorted (segmented)
 constexpr int64_t kCsortSegExtra = 128;
 constexpr int64_t kCsortSegHeavy = 8;  // entries of one row in a chunk that make it a run
+constexpr double kPartSlack = 1.25;    // widest column part / (n / H) when balancing entries
+// Row-partition weight of a crowded row's entries (ones that land >= 8 to a
+// chunk, so their chunks are segmented): a segmented chunk cost 0.164 us on
+// top of a plain one's ~0.37 us in the per-workgroup fit of c5r (entries,
+// gather quad-sectors, segmented chunks; r^2 0.92, r04a).
+constexpr int32_t kWUnit = 16, kWCrowded = 23;
 
 struct CsEnt {
   uint32_t col, slot, k;
@@ -78,7 +84,35 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   const size_t sv = dtype_size(dtype);
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX
                          : (s.tune.csort_long > 0 ? s.tune.csort_long : kLongRow);
-  auto part_of = [&](int64_t c) { return (int)((c * H) / n); };  // c in part floor(c*H/n)
+  // Column parts: [pb[h], pb[h+1]).  Equal widths, or (Tuning.csort_balance
+  // >= 0, the default) boundaries at equal shares of the entries, each part's
+  // width kept within kPartSlack of n / H: an RCM ordering concentrates a
+  // power-law matrix's entries in the upper columns (c5r: 59 % in the upper
+  // half), and equal widths gave that half's workgroups 1.42x the entries
+  // (per-workgroup timelines, profiles/r04a_csort_trace_wg.jsonl).
+  std::vector<int64_t> pb((size_t)H + 1, 0);
+  for (int h = 0; h <= H; ++h) pb[(size_t)h] = (n * h + H - 1) / H;  // c in part floor(c*H/n)
+  if (H > 1 && tn.csort_balance >= 0) {
+    std::vector<int64_t> colcnt((size_t)n + 1, 0);
+    for (int64_t k = 0; k < rp[m]; ++k) ++colcnt[(size_t)col[k]];
+    const int64_t tot = rp[m];
+    int64_t acc = 0, c = 0;
+    for (int h = 1; h < H; ++h) {
+      const int64_t target = tot * h / H;
+      while (c < n && acc + colcnt[(size_t)c] <= target) acc += colcnt[(size_t)c++];
+      const int64_t eq = (n * h + H - 1) / H;
+      const int64_t slack = (int64_t)((kPartSlack - 1.0) * (double)(n / H));
+      const int64_t lo = std::max(pb[(size_t)h - 1] + 1, eq - slack), hi = std::max(lo, eq + slack);
+      pb[(size_t)h] = std::min(std::max(c, lo), hi);
+    }
+  }
+  std::vector<uint8_t> part_tab;
+  if (H > 1) {
+    part_tab.assign((size_t)n, 0);
+    for (int h = 0; h < H; ++h)
+      std::fill(part_tab.begin() + pb[(size_t)h], part_tab.begin() + pb[(size_t)h + 1], (uint8_t)h);
+  }
+  auto part_of = [&](int64_t c) { return H > 1 ? (int)part_tab[(size_t)c] : 0; };
   // long rows and their slices (per part, kCsortSlice nonzeros each)
   std::vector<int32_t> lrow, lcs(1, 0);
   std::vector<std::vector<uint32_t>> slice_k;  // source nonzeros per slice
@@ -100,8 +134,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     lcs.push_back((int32_t)slice_k.size());
   }
   const int64_t n_slices = (int64_t)slice_k.size();
-  // Row blocks PER COLUMN PART.  Part h is a fixed slice of x,
-  // [ceil(n h / H), ceil(n (h + 1) / H)), and workgroup j works on part
+  // Row blocks PER COLUMN PART.  Part h is a fixed slice of x, [pb[h],
+  // pb[h+1]) (above), and workgroup j works on part
   // j % H: under round-robin dispatch (workgroup j on XCD j % 8;
   // tools/xcd_map_probe.hip records it per box) every XCD sweeps one slice,
   // which its 4 MiB L2 keeps for all its CUs.  Each part has its OWN row
@@ -115,20 +149,52 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   const int64_t reserve = n_slices / nb0 + 2;
   const int64_t row_cap = max_slots - 1 - reserve;
   if (row_cap < 64) return HSPMV_OK;  // too many slices for the LDS: not this path
-  std::vector<int32_t> cnt((size_t)(H * m), 0);  // [h][r]: row r's in-kernel nonzeros in part h
-  {
-    const int ntc = (int)std::max<int64_t>(1, std::min<int64_t>(16, m / 65536));
+  // [h][r]: row r's in-kernel nonzeros in part h, then its partition weight
+  std::vector<int32_t> cnt((size_t)(H * m), 0);
+  std::vector<int32_t> cmin((size_t)(H * m), INT32_MAX), cmax((size_t)(H * m), -1);
+  std::vector<int64_t> tot_part((size_t)H, 0);
+  const int ntc = (int)std::max<int64_t>(1, std::min<int64_t>(16, m / 65536));
+  auto par_rows = [&](auto &&body) {
     std::vector<std::thread> th;
-    for (int t = 0; t < ntc; ++t)
-      th.emplace_back([&, t]() {
-        for (int64_t r = m * t / ntc; r < m * (t + 1) / ntc; ++r) {
-          if (rp[r + 1] - rp[r] > long_t) continue;
-          for (int32_t k = rp[r]; k < rp[r + 1]; ++k) ++cnt[(size_t)(part_of(col[k]) * m + r)];
-        }
-      });
+    for (int t = 0; t < ntc; ++t) th.emplace_back([&, t]() { body(m * t / ntc, m * (t + 1) / ntc); });
     for (auto &x : th) x.join();
+  };
+  par_rows([&](int64_t r0, int64_t r1) {
+    for (int64_t r = r0; r < r1; ++r) {
+      if (rp[r + 1] - rp[r] > long_t) continue;
+      for (int32_t k = rp[r]; k < rp[r + 1]; ++k) {
+        const size_t i = (size_t)(part_of(col[k]) * m + r);
+        ++cnt[i];
+        cmin[i] = std::min(cmin[i], col[k]);
+        cmax[i] = std::max(cmax[i], col[k]);
+      }
+    }
+  });
+  for (int h = 0; h < H; ++h)
+    for (int64_t r = 0; r < m; ++r) tot_part[(size_t)h] += cnt[(size_t)(h * m + r)];
+  {
+    // crowded rows: entries per chunk ~ k * min(1, chunk span / row span),
+    // chunk span = the columns one chunk of a block covers
+    std::vector<double> cspan((size_t)H, 0.0);
+    for (int h = 0; h < H; ++h)
+      cspan[(size_t)h] = tot_part[(size_t)h] ? (double)C * (double)(pb[(size_t)h + 1] - pb[(size_t)h]) *
+                                                   (double)nb0 / (double)tot_part[(size_t)h]
+                                             : 0.0;
+    const bool weigh = tn.csort_balance >= 0;
+    par_rows([&](int64_t r0, int64_t r1) {
+      for (int h = 0; h < H; ++h)
+        for (int64_t r = r0; r < r1; ++r) {
+          const size_t i = (size_t)(h * m + r);
+          const int32_t k = cnt[i];
+          double per_chunk = 0.0;
+          if (k > 0) per_chunk = (double)k * std::min(1.0, cspan[(size_t)h] / (double)(cmax[i] - cmin[i] + 1));
+          cnt[i] = k * (weigh && per_chunk >= (double)kCsortSegHeavy ? kWCrowded : kWUnit);
+        }
+    });
   }
-  // Greedy cuts at `target` nonzeros or row_cap rows; the target is the
+  std::vector<int32_t>().swap(cmin);
+  std::vector<int32_t>().swap(cmax);
+  // Greedy cuts at `target` weight or row_cap rows; the target is the
   // smallest that yields at most nb0 blocks (one block more would run a
   // second round of workgroups on one CU and double the launch).
   auto cut = [&](int h, int64_t target, std::vector<int32_t> *out) -> int64_t {
@@ -150,7 +216,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   std::vector<std::vector<int32_t>> brh((size_t)H);
   int64_t NB = 0;
   for (int h = 0; h < H; ++h) {
-    int64_t tot_h = 0;
+    int64_t tot_h = 0;  // the part's weight
     for (int64_t r = 0; r < m; ++r) tot_h += cnt[(size_t)(h * m + r)];
     int64_t lo = std::max<int64_t>(1, (tot_h + nb0 - 1) / nb0), hi = std::max<int64_t>(lo, tot_h + 1);
     if (cut(h, lo, nullptr) > nb0) {

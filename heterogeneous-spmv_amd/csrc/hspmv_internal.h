@@ -71,8 +71,11 @@ struct Tuning {
   int csort_seg_extra = 0;               // serialised same-slot lanes that flag a chunk (0: default)
   int csort_trace = 0;                   // per-workgroup timestamps (hspmv_diag_csort_trace)
   int csort_long = 0;                    // rows above this many nonzeros are sliced (0: kLongRow)
+  int csort_balance = 0;                 // -1: equal-width column parts, nnz-balanced rows (r03)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
+  int csr3_py = 0;                       // CSR3 + x dictionaries: blocks per workgroup with
+                                         // the y slice staged in LDS (0: off)
 };
 
 constexpr int kC16Shift = 8;  // 256 nonzeros per column-base block
@@ -139,6 +142,9 @@ struct DevPlan {
   const int32_t *xd_blk = nullptr;
   const void *xd_runs = nullptr;
   int32_t xd_lds_bytes = 0;
+  // A/B (Tuning.csr3_py): dictionary blocks per workgroup of the CSR3 kernel
+  // that stages its y slice in LDS (hspmv_csr3_py), and the largest slice
+  int32_t py_bpw = 0, py_rows = 0;
   // x slabs (irregular gathers, x larger than an XCD's L2): the columns are
   // cut into n_slabs equal ranges and the row kernel runs
   // once per slab over a slab-major copy of the matrix -- pass b reads rows

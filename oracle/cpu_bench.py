@@ -97,6 +97,23 @@ def l3_places(cpus) -> list:
     return out
 
 
+def cpu_stat() -> dict:
+    """The cgroup's CPU accounting (cpu.stat): throttled periods and time."""
+    out = {}
+    try:
+        for line in Path("/sys/fs/cgroup/cpu.stat").read_text().splitlines():
+            k, v = line.split()
+            out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def throttled(before: dict, after: dict) -> dict:
+    return {k: after.get(k, 0) - before.get(k, 0)
+            for k in ("nr_periods", "nr_throttled", "throttled_usec") if k in after}
+
+
 def timing(nnz: int, samples: np.ndarray) -> dict:
     tmin, tmax = float(samples.min()), float(samples.max())
     tavg, tmed = float(samples.mean()), float(np.median(samples))
@@ -167,7 +184,13 @@ def run(d: Path, budget_s: float, threads: int = 0, bind: bool = True, tried: bo
     res = {}
     for sched in ("static", "guided"):  # run_norm.py:18,66 / run_cuda_new.py:79
         oracle.set_schedule(sched, threads)
-        res[sched] = timing(nnz, oracle.time_spmv_samples(lrp, lci, lval, x, 5, runs))
+        c0 = cpu_stat()
+        smp = oracle.time_spmv_samples(lrp, lci, lval, x, 5, runs)
+        res[sched] = timing(nnz, smp)
+        res[sched]["cgroup_throttling"] = throttled(c0, cpu_stat())
+        # share of runs within 10 % / 50 % of TimeMin
+        res[sched]["runs_within_10pct_of_min"] = round(float(np.mean(smp <= 1.1 * smp.min())), 3)
+        res[sched]["runs_within_50pct_of_min"] = round(float(np.mean(smp <= 1.5 * smp.min())), 3)
     st = res["static"]
     legs[int(threads)] = dict(st, within_quota=True, note="reported leg")
     dt = "fp64" if val.dtype == np.float64 else "fp32"
@@ -187,7 +210,8 @@ def run(d: Path, budget_s: float, threads: int = 0, bind: bool = True, tried: bo
                       f"5 warm-ups + {runs} timed runs (spmv-csr/spmv.c:164-185 protocol), "
                       f"value = 2 nnz / TimeMin"),
            **{k: st[k] for k in ("time_min_s", "time_avg_s", "time_max_s", "median_s", "avg_over_min",
-                                 "gflops_from_median", "gflops_from_avg")},
+                                 "gflops_from_median", "gflops_from_avg", "cgroup_throttling",
+                                 "runs_within_10pct_of_min", "runs_within_50pct_of_min")},
            "host": hw, "wait_policy": policy, "threads_tried": legs,
            "guided": {"gflops": res["guided"]["gflops_from_min"],
                       "gflops_from_median": res["guided"]["gflops_from_median"],
