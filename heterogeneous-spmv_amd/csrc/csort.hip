@@ -290,34 +290,36 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
 // y[r] = part[r] + part[m + r] + ... (parts in order), except long rows:
 // blocks past the row blocks sum each long row's slices (one wave per row,
 // fixed lane assignment and shuffle tree).
-// R2: two rows per thread with 16-byte partial loads (m even, so every
-// part's rows stay 16-byte aligned).
-template <typename T, typename S, bool R2>
+// R rows per thread (1, 2, 4): R-element partial loads (16 / 32 bytes for
+// R = 2 / 4; m a multiple of R keeps every part's rows aligned).
+template <typename T, typename S, int R>
 __global__ __launch_bounds__(256) void hspmv_csort_finish(
     int64_t m, int32_t H, int64_t row_blocks, const S *__restrict__ part,
     const uint32_t *__restrict__ long_mask, int32_t n_long, const int32_t *__restrict__ long_row,
     const int32_t *__restrict__ long_cs, const S *__restrict__ spart, T *__restrict__ y) {
   if ((int64_t)blockIdx.x < row_blocks) {
-    if constexpr (R2) {
-      typedef S s2 __attribute__((ext_vector_type(2)));
-      typedef T t2 __attribute__((ext_vector_type(2)));
-      const int64_t r = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+    if constexpr (R > 1) {
+      typedef S sr __attribute__((ext_vector_type(R)));
+      typedef T tr __attribute__((ext_vector_type(R)));
+      const int64_t r = R * ((int64_t)blockIdx.x * 256 + threadIdx.x);
       if (r >= m) return;
-      s2 s = *reinterpret_cast<const s2 *>(part + r);
+      sr s = *reinterpret_cast<const sr *>(part + r);
       for (int32_t h = 1; h < H; ++h) {
-        const s2 q = *reinterpret_cast<const s2 *>(part + (int64_t)h * m + r);
-        s.x += q.x;
-        s.y += q.y;
+        const sr q = *reinterpret_cast<const sr *>(part + (int64_t)h * m + r);
+#pragma unroll
+        for (int j = 0; j < R; ++j) s[j] += q[j];
       }
-      const uint32_t lm = long_mask ? (long_mask[r >> 5] >> (r & 31)) & 3u : 0u;
+      // R <= 4 rows never straddle a 32-row mask word (r is a multiple of R)
+      const uint32_t lm = long_mask ? (long_mask[r >> 5] >> (r & 31)) & ((1u << R) - 1u) : 0u;
       if (lm == 0u) {
-        t2 o;
-        o.x = (T)s.x;
-        o.y = (T)s.y;
-        *reinterpret_cast<t2 *>(y + r) = o;
+        tr o;
+#pragma unroll
+        for (int j = 0; j < R; ++j) o[j] = (T)s[j];
+        *reinterpret_cast<tr *>(y + r) = o;
       } else {  // a long row's y comes from its slices
-        if (!(lm & 1u)) y[r] = (T)s.x;
-        if (!(lm & 2u)) y[r + 1] = (T)s.y;
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+          if (!((lm >> j) & 1u)) y[r + j] = (T)s[j];
       }
       return;
     } else {
@@ -338,6 +340,14 @@ __global__ __launch_bounds__(256) void hspmv_csort_finish(
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
   if (lane == 0) y[long_row[j]] = (T)s;
+}
+
+template <typename T, typename S, int R>
+void launch_finish(const DevCsort &c, const S *part, const S *spart, T *y, hipStream_t st) {
+  const int64_t lb = ((int64_t)c.n_long + 3) / 4;
+  const int64_t rb = (c.m / R + 255) / 256;
+  hipLaunchKernelGGL((hspmv_csort_finish<T, S, R>), dim3((unsigned)(rb + lb)), dim3(256), 0, st, c.m, c.H,
+                     rb, part, c.long_mask, c.n_long, c.long_row, c.long_cs, spart, y);
 }
 
 template <typename T, typename S, int U, bool NT, bool PF, bool WIDE>
@@ -366,16 +376,16 @@ hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || c.direct) return e;
-  const int64_t lb = ((int64_t)c.n_long + 3) / 4;
-  if (c.wide && c.m % 2 == 0) {
-    const int64_t rb = (c.m / 2 + 255) / 256;
-    hipLaunchKernelGGL((hspmv_csort_finish<T, S, true>), dim3((unsigned)(rb + lb)), dim3(256), 0, st,
-                       c.m, c.H, rb, part, c.long_mask, c.n_long, c.long_row, c.long_cs, spart, y);
-  } else {
-    const int64_t rb = (c.m + 255) / 256;
-    hipLaunchKernelGGL((hspmv_csort_finish<T, S, false>), dim3((unsigned)(rb + lb)), dim3(256), 0, st,
-                       c.m, c.H, rb, part, c.long_mask, c.n_long, c.long_row, c.long_cs, spart, y);
-  }
+  // rows per finishing thread: 4 (32-byte partial loads; C5 104.4 -> 103.5
+  // us, c5r 110.0 -> 107.8 against 2, r04c/ab_c5_fin_rows.jsonl), fewer when
+  // m is not a multiple; c.fin_rows overrides (A/B)
+  const int fr = c.fin_rows > 0 ? c.fin_rows : 4;
+  if (fr >= 4 && c.m % 4 == 0)
+    launch_finish<T, S, 4>(c, part, spart, y, st);
+  else if (fr >= 2 && c.m % 2 == 0)
+    launch_finish<T, S, 2>(c, part, spart, y, st);
+  else
+    launch_finish<T, S, 1>(c, part, spart, y, st);
   return hipGetLastError();
 }
 

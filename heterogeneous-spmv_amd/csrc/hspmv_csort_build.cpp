@@ -35,7 +35,8 @@ constexpr int32_t kCsortSlice = 2048;
 // lanes in all is stored slot-sorted (segmented)
 constexpr int64_t kCsortSegExtra = 128;
 constexpr int64_t kCsortSegHeavy = 8;  // entries of one row in a chunk that make it a run
-constexpr double kPartSlack = 1.25;    // widest column part / (n / H) when balancing entries
+constexpr double kPartSlack = 1.25;    // widest column part / (n / H) when balancing cost
+constexpr double kSweepPerRowBlock = 0.13;  // a column's sweep cost, in entries, per row block
 // Row-partition weight of a crowded row's entries (ones that land >= 8 to a
 // chunk, so their chunks are segmented): a segmented chunk cost 0.164 us on
 // top of a plain one's ~0.37 us in the per-workgroup fit of c5r (entries,
@@ -85,21 +86,29 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX
                          : (s.tune.csort_long > 0 ? s.tune.csort_long : kLongRow);
   // Column parts: [pb[h], pb[h+1]).  Equal widths, or (Tuning.csort_balance
-  // >= 0, the default) boundaries at equal shares of the entries, each part's
-  // width kept within kPartSlack of n / H: an RCM ordering concentrates a
-  // power-law matrix's entries in the upper columns (c5r: 59 % in the upper
-  // half), and equal widths gave that half's workgroups 1.42x the entries
-  // (per-workgroup timelines, profiles/r04a_csort_trace_wg.jsonl).
+  // >= 0, the default) boundaries at equal shares of the parts' COST, each
+  // part's width kept within kPartSlack of n / H.  A workgroup's time is
+  // ~alpha per entry + beta per column of its part (the x sweep): from the
+  // per-workgroup timelines of c5r (profiles/r04c/csort_trace_wg*.jsonl),
+  // alpha = 2.5e-4 us, beta = 3.0-3.4e-5 us per fp32 column, so a column
+  // weighs kSweepPerRowBlock * (row blocks) entries (x 2 * 8 / 12 for fp64
+  // x and entries).  An RCM ordering concentrates a power-law matrix's
+  // entries in the upper columns (c5r: 59 % in the upper half): equal widths
+  // gave that half's workgroups 1.42x the entries (123.4 us), equal entries
+  // over-corrected onto the wider lower part (108.8 us, its sweep 43 % wider).
   std::vector<int64_t> pb((size_t)H + 1, 0);
   for (int h = 0; h <= H; ++h) pb[(size_t)h] = (n * h + H - 1) / H;  // c in part floor(c*H/n)
   if (H > 1 && tn.csort_balance >= 0) {
     std::vector<int64_t> colcnt((size_t)n + 1, 0);
     for (int64_t k = 0; k < rp[m]; ++k) ++colcnt[(size_t)col[k]];
-    const int64_t tot = rp[m];
-    int64_t acc = 0, c = 0;
+    const double nb_part = (double)std::max<int64_t>(1, (int64_t)cus * bpc / H);
+    const double wcol = kSweepPerRowBlock * nb_part * (dtype == HSPMV_F64 ? 2.0 * 8.0 / 12.0 : 1.0);
+    const double tot = (double)rp[m] + wcol * (double)n;
+    double acc = 0.0;
+    int64_t c = 0;
     for (int h = 1; h < H; ++h) {
-      const int64_t target = tot * h / H;
-      while (c < n && acc + colcnt[(size_t)c] <= target) acc += colcnt[(size_t)c++];
+      const double target = tot * h / H;
+      while (c < n && acc + (double)colcnt[(size_t)c] + wcol <= target) acc += (double)colcnt[(size_t)c++] + wcol;
       const int64_t eq = (n * h + H - 1) / H;
       const int64_t slack = (int64_t)((kPartSlack - 1.0) * (double)(n / H));
       const int64_t lo = std::max(pb[(size_t)h - 1] + 1, eq - slack), hi = std::max(lo, eq + slack);
@@ -507,6 +516,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   if (tn.csort_pf >= 0) c.prefetch = tn.csort_pf != 0;
   c.slot32 = slot32;
   c.wide = wide;
+  c.fin_rows = tn.csort_fin_rows;
   c.m = m;
   c.lds_bytes = (int32_t)(slot_bytes * max_slots_used);
   c.blk_c = s.d_cs_blk_c;

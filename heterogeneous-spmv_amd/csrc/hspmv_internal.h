@@ -72,10 +72,9 @@ struct Tuning {
   int csort_trace = 0;                   // per-workgroup timestamps (hspmv_diag_csort_trace)
   int csort_long = 0;                    // rows above this many nonzeros are sliced (0: kLongRow)
   int csort_balance = 0;                 // -1: equal-width column parts, nnz-balanced rows (r03)
+  int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
-  int csr3_py = 0;                       // CSR3 + x dictionaries: blocks per workgroup with
-                                         // the y slice staged in LDS (0: off)
 };
 
 constexpr int kC16Shift = 8;  // 256 nonzeros per column-base block
@@ -102,6 +101,7 @@ struct DevCsort {
   bool prefetch = false;  // next chunk's entries loaded during this chunk's gathers
   bool slot32 = false;    // fp32 LDS row slots and partials (fp32 data; A/B)
   bool wide = false;      // 16-byte entry loads (host-interleaved layout)
+  int32_t fin_rows = 0;   // rows per finishing-pass thread (0: 4, or the most m allows)
   int64_t m = 0;
   int32_t lds_bytes = 0;
   const int32_t *blk_c = nullptr, *blk_r = nullptr, *blk_v = nullptr, *vslice = nullptr;
@@ -142,9 +142,6 @@ struct DevPlan {
   const int32_t *xd_blk = nullptr;
   const void *xd_runs = nullptr;
   int32_t xd_lds_bytes = 0;
-  // A/B (Tuning.csr3_py): dictionary blocks per workgroup of the CSR3 kernel
-  // that stages its y slice in LDS (hspmv_csr3_py), and the largest slice
-  int32_t py_bpw = 0, py_rows = 0;
   // x slabs (irregular gathers, x larger than an XCD's L2): the columns are
   // cut into n_slabs equal ranges and the row kernel runs
   // once per slab over a slab-major copy of the matrix -- pass b reads rows

@@ -644,15 +644,6 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
       s.dp.xd_blk = s.d_xd_blk;
       s.dp.xd_runs = s.d_xd_runs;
       s.dp.xd_lds_bytes = s.xd_lds_bytes;
-      if (s.tune.csr3_py > 0 && s.xd_shape == kCsr3 && s.plan.waves_per_block == 4) {
-        // the largest y slice of bpw consecutive 4-task blocks
-        const int64_t nt = (int64_t)s.h_tasks.size() - 1, step = 4LL * s.tune.csr3_py;
-        int32_t rows = 0;
-        for (int64_t t = 0; t < nt; t += step)
-          rows = std::max(rows, s.h_tasks[(size_t)std::min(nt, t + step)] - s.h_tasks[(size_t)t]);
-        s.dp.py_bpw = s.tune.csr3_py;
-        s.dp.py_rows = rows;
-      }
       // index bytes: 2 instead of 4 per in-kernel nonzero, plus the tables;
       // x: the staged entries instead of the distinct columns
       const double sv = (double)dtype_size(dtype);

@@ -673,84 +673,6 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
 #endif
 }
 
-// CSR3 with x dictionaries, y staged per workgroup (A/B: Tuning.csr3_py =
-// blocks per workgroup).  Writes interleaved with the read
-// stream cost C3 ~9 us (the L1's TA data stall, bw_probe6); here workgroup g
-// runs the dictionary blocks [g*bpw, (g+1)*bpw) one after the other, its
-// waves' row sums go to an LDS copy of the workgroup's y slice, and the slice
-// is written once, with 16-byte stores, after its last block.  The sums and
-// so every y bit are the hspmv_csr3 kernel's.  Split rows' y entries are
-// left to the split-row kernels, which run after this one.
-template <typename T, bool NT, int U, bool PF, int W>
-__global__ __launch_bounds__(W * 64) void hspmv_csr3_py(
-    int32_t n_tasks, int32_t bpw, int32_t xd_bytes, int32_t long_t,
-    const int32_t *__restrict__ task_start, XDict xd, const int32_t *__restrict__ rp, ColSrc cs,
-    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
-  __shared__ T lds[W * kWave * U];
-  extern __shared__ __attribute__((aligned(16))) unsigned char xdyn[];  // xs, then the y slice
-  T *xs = reinterpret_cast<T *>(xdyn);
-  T *ys = reinterpret_cast<T *>(xdyn + xd_bytes);
-  const int wid = threadIdx.x >> 6;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t b0 = (int64_t)blockIdx.x * bpw;
-  const int64_t nblk = ((int64_t)n_tasks + W - 1) / W;
-  const int64_t b1 = min<int64_t>(b0 + bpw, nblk);
-  if (b0 >= b1) return;  // block-uniform
-  const int64_t t_end = b1 * W < (int64_t)n_tasks ? b1 * W : (int64_t)n_tasks;
-  const int32_t row0 = task_start[b0 * W];
-  const int32_t row1 = task_start[t_end];
-  T *my = lds + wid * kWave * U;
-  const XWin<T> win{xs, 0, 0};
-  for (int64_t b = b0; b < b1; ++b) {  // block-uniform
-    stage_xdict<T, W * 64>(xs, x, xd, b, threadIdx.x);
-    const int64_t t = b * W + wid;
-    if (t < n_tasks) {
-      const int64_t tb = sload_i64(task_start, (uint64_t)t * 4u);
-      const int32_t r0 = (int32_t)tb, r1 = (int32_t)(tb >> 32);
-      if (r0 < r1) {
-        int32_t beg, end;
-        group_bounds(rp, r0, min(r0 + kWave, r1), lane, beg, end);
-        for (int32_t g0 = r0; g0 < r1; g0 += kWave) {
-          const int32_t g1 = min(g0 + kWave, r1);
-          int32_t nbeg = 0, nend = 0;
-          if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
-          wave_rows<T, NT, U, PF, 0, false, true, HSPMV_COOP_GROUPS != 0>(
-              g0, g1, beg, end, long_t, cs, val, x, ys - row0, my, lane, win, false, false, 0);
-          beg = nbeg;
-          end = nend;
-        }
-      }
-    }
-    __syncthreads();  // the next block restages xs
-  }
-  // the slice, 16 bytes per store where aligned, streamed past the caches
-  const int32_t nr = row1 - row0;
-  constexpr int V = 16 / (int)sizeof(T);
-  const int32_t head = min(nr, (int32_t)((V - (row0 % V)) % V));
-  for (int32_t i = threadIdx.x; i < head; i += W * 64)
-    if (rp[row0 + i + 1] - rp[row0 + i] <= long_t) __builtin_nontemporal_store(ys[i], y + row0 + i);
-  typedef T tv __attribute__((ext_vector_type(V)));
-  const int32_t nv = (nr - head) / V;
-  for (int32_t i = threadIdx.x; i < nv; i += W * 64) {
-    const int32_t r = head + i * V;
-    bool plain = true;
-#pragma unroll
-    for (int j = 0; j < V; ++j) plain &= rp[row0 + r + j + 1] - rp[row0 + r + j] <= long_t;
-    if (plain) {
-      tv v;
-#pragma unroll
-      for (int j = 0; j < V; ++j) v[j] = ys[r + j];
-      __builtin_nontemporal_store(v, reinterpret_cast<tv *>(y + row0 + r));
-    } else {
-#pragma unroll
-      for (int j = 0; j < V; ++j)
-        if (rp[row0 + r + j + 1] - rp[row0 + r + j] <= long_t) y[row0 + r + j] = ys[r + j];
-    }
-  }
-  for (int32_t i = head + nv * V + threadIdx.x; i < nr; i += W * 64)
-    if (rp[row0 + i + 1] - rp[row0 + i] <= long_t) __builtin_nontemporal_store(ys[i], y + row0 + i);
-}
-
 // ------------------------------------------------------------------ launchers
 
 inline ColSrc col_src(const DevCSR &A) {
@@ -811,15 +733,6 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
                      dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,     \
                      (int32_t)p.y_nt, p.carry, dp.task_start, xw, xd, A.row_ptr, cs, val, x, y)
   if constexpr (XD) {  // packed tasks only (4 or 8 per block)
-    if (dp.py_bpw > 0 && p.waves_per_block == 4) {  // A/B: y staged per workgroup
-      const unsigned nblk = (unsigned)((dp.n_tasks + 3) / 4);
-      const unsigned grid = (nblk + (unsigned)dp.py_bpw - 1) / (unsigned)dp.py_bpw;
-      hipLaunchKernelGGL((hspmv_csr3_py<T, NT, U, PF, 4>), dim3(grid), dim3(256),
-                         (unsigned)dp.xd_lds_bytes + (unsigned)dp.py_rows * (unsigned)sizeof(T), st,
-                         dp.n_tasks, dp.py_bpw, dp.xd_lds_bytes, dp.long_t, dp.task_start, xd, A.row_ptr,
-                         cs, val, x, y);
-      return;
-    }
     if (p.waves_per_block == 8)
       HSPMV_CSR3(8, false, false, true);
     else

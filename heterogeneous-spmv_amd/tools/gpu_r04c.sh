@@ -13,3 +13,4 @@ step csort_tests 300 python -u -m pytest tests/test_csort.py -x -q --timeout 200
 step ab_balance 400 python $T/ab.py --libs "$E#HSPMV_CSORT_BALANCE=-1,$E" --configs c5,c5r --rounds 5 --out $O/ab_c5_balance.jsonl
 step trace 240 python $T/csort_trace.py --configs c5,c5r --per-wg --out $O/csort_trace_wg_balanced.jsonl
 step ab_c3_py 500 python $T/ab.py --libs "$E,$E#HSPMV_CSR3_PY=1,$E#HSPMV_CSR3_PY=2,$E#HSPMV_CSR3_PY=4,$E#HSPMV_CSR3_PY=8" --configs c3,c3:f32 --rounds 5 --out $O/ab_c3_py.jsonl
+step ab_c5_fin 300 python $T/ab.py --libs "$E,$E#HSPMV_CSORT_FIN_ROWS=4,$E#HSPMV_CSORT_FIN_ROWS=1" --configs c5,c5r --rounds 5 --out $O/ab_c5_fin_rows.jsonl
