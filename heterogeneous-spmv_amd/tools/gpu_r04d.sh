@@ -1,6 +1,7 @@
 #!/bin/bash
-# GPU-box pass (round 4 d): cost-balanced csort column parts (A/B against
-# equal widths, one process), the timelines with it, csort tests.
+# GPU-box pass (round 4 d): csort paired row blocks (in-launch combine of
+# the two column parts) and cost-balanced parts: tests, one-process A/Bs,
+# per-workgroup timelines.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/r04d; mkdir -p $O
 cd $R; T=heterogeneous-spmv_amd/tools; E=heterogeneous-spmv_amd/build/diagenv/libhspmv.so
 step() {  # step NAME SECONDS CMD...
@@ -9,6 +10,6 @@ step() {  # step NAME SECONDS CMD...
   echo "   rc=$rc"; tail -4 $O/$name.log | cut -c1-400
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stop: $name rc=$rc"; exit $rc; fi
 }
-step csort_tests 300 python -u -m pytest tests/test_csort.py -x -q --timeout 200 --timeout-method thread
-step ab_balance 400 python $T/ab.py --libs "$E#HSPMV_CSORT_BALANCE=-1,$E" --configs c5,c5r --rounds 7 --out $O/ab_c5_balance_cost.jsonl
+step csort_tests 300 python -u -m pytest tests/test_csort.py tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "csort or c5"
+step ab_pair 400 python $T/ab.py --libs "$E#HSPMV_CSORT_PAIR=-1#HSPMV_CSORT_BALANCE=-1,$E#HSPMV_CSORT_PAIR=-1,$E" --configs c5,c5r --rounds 7 --out $O/ab_c5_pair_balance.jsonl
 step trace 240 python $T/csort_trace.py --configs c5,c5r --per-wg --out $O/csort_trace_wg_cost.jsonl

@@ -67,6 +67,32 @@ def test_c3_shards_cover_the_matrix_on_ssr_boundaries():
         assert rows == A.m
 
 
+def test_cpu_baseline_runs_in_its_own_process(tmp_path):
+    """bench.py's CPU legs (oracle/cpu_bench.py) on a small matrix: a process
+    of its own, the reference protocol's min / median / avg, the reported
+    team one thread under the cgroup quota (or the physical cores), the
+    cgroup's throttling counters, and the reference's own omp_spmv beside
+    it when oracle/_ref was built."""
+    sys.path.insert(0, str(REPO))
+    import bench
+    from hspmv import gen
+    A = gen.laplace2d(300, 300)
+    x = gen.rand_x(A.n, 42)
+    c = bench.cpu_baseline(A, x, 0.5)
+    assert c["kind"] == "port" and c["unit"] == "GFLOP/s" and c["value"] > 0
+    assert abs(c["value"] - 2 * A.nnz / c["time_min_s"] * 1e-9) < 1e-2 * c["value"]
+    assert c["time_min_s"] <= c["median_s"] <= c["time_max_s"]
+    assert c["threads_tried"][str(c["cores"])]["note"] == "reported leg"
+    q = c["cgroup_cpu_quota"]
+    assert c["cores"] == (max(1, min(c["host"]["physical_cores"] or c["host"]["affinity_cpus"],
+                                     c["host"]["affinity_cpus"], int(q) - 1)) if q else c["cores"])
+    assert "a process of its own" in c["cores_note"] and f"nnz={A.nnz}" in c["sample"]
+    assert 0.0 <= c["runs_within_10pct_of_min"] <= 1.0
+    if (REPO / "oracle" / "_ref" / "libref_spmvcsr.so").exists():
+        r = c["reference_f32"]
+        assert r["kind"] == "reference" and r["value"] > 0 and r["cores"] == c["cores"]
+
+
 @pytest.mark.gpu
 def test_bench_json_line_contract():
     env = dict(os.environ, PYTHONUNBUFFERED="1")
