@@ -339,7 +339,13 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
       return;
     }
     if (threadIdx.x == 0) {
-      while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+      // bounded (200 ms of the 100 MHz s_memrealtime clock): a partner that
+      // never publishes -- counters left behind by an aborted launch -- must
+      // cost a wrong y on that block, never a hung launch; the reset below
+      // then repairs the counters for the next SpMV
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+             __builtin_amdgcn_s_memrealtime() - t0 < 20000000ull)
         __builtin_amdgcn_s_sleep(2);
       __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ready, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
