@@ -209,6 +209,46 @@ def test_csort_segmented_chunks_for_contiguous_hub_rows(dtype):
     check(B, gen.rand_x(B.n, 3).astype(dtype), y)
 
 
+def _uniform_with_long_rows(dtype, seed=13, m=600_000, n=1_500_000):
+    """Short rows over random columns (every row splits evenly over the two
+    column parts, so the parts share one row partition: paired blocks) plus
+    long rows cut into slices, first / last / adjacent rows among them."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(2, 16, m)
+    for r, ln in [(0, 9000), (1, 4097), (777, 30_000), (778, 5000), (m - 1, 12_000)]:
+        lens[r] = ln
+    rp = np.concatenate([[0], np.cumsum(lens)])
+    # columns sorted within each row (duplicates allowed: summed like any)
+    key = np.repeat(np.arange(m, dtype=np.int64), lens) * n + rng.integers(0, n, rp[-1])
+    ci = (np.sort(key) % n).astype(np.int32)
+    return hspmv.CsrMatrix(m, n, rp, ci, rng.uniform(-1, 1, rp[-1]).astype(dtype))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_csort_paired_blocks_and_slice_combine(dtype):
+    """Paired row blocks: the two column parts' workgroups of a row block
+    combine in the launch (the second adds the first's published sums), and
+    a long row's slices are added by the workgroup that publishes the last
+    one -- no finishing pass.  Every SpMV of a back-to-back run is checked
+    (which workgroup arrives second changes from launch to launch), and the
+    counters reset themselves between launches."""
+    A = _uniform_with_long_rows(dtype)
+    x = gen.rand_x(A.n, 21).astype(dtype)
+    lens = np.diff(A.row_ptr)
+    with hspmv.SpMV(A, kernel="csort") as op:
+        info = op.info
+        assert info["csort_parts"] == 2 and info["csort_paired"] == 1, info
+        assert info["n_split_rows"] == int((lens > 4096).sum())
+        op.set_x(x)
+        for _ in range(10):
+            op.spmv()
+            check(A, x, op.get_y())
+        x2 = gen.rand_x(A.n, 22).astype(dtype)  # a new x: nothing stale from the last launch
+        op.set_x(x2)
+        op.spmv()
+        check(A, x2, op.get_y())
+
+
 def test_csort_rcm_powerlaw_matches_oracle():
     A = gen.powerlaw(150_000, seed=21, dtype=np.float32, rcm=True)
     x = gen.rand_x(A.n, 4).astype(np.float32)
