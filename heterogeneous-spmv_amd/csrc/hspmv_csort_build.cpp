@@ -37,7 +37,9 @@ constexpr int64_t kCsortSegExtra = 128;
 constexpr int64_t kCsortSegHeavy = 8;  // entries of one row in a chunk that make it a run
 constexpr double kPartSlack = 1.25;    // widest column part / (n / H) when balancing cost
 constexpr double kSweepPerRowBlock = 0.13;  // a column's sweep cost, in entries, per row block
-constexpr double kPairSlack = 1.04;         // paired blocks: largest part share / the part's mean
+// paired blocks: largest part share of a block / the part's mean (C5's
+// power-law rows split over the parts unevenly enough for 1.047 at best)
+constexpr double kPairSlack = 1.06;
 // Row-partition weight of a crowded row's entries (ones that land >= 8 to a
 // chunk, so their chunks are segmented): a segmented chunk cost 0.164 us on
 // top of a plain one's ~0.37 us in the per-workgroup fit of c5r (entries,
