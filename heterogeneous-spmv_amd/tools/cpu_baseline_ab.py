@@ -43,6 +43,7 @@ def main():
     np.save(d / "x.npy", gen.rand_x(A.n, 42, dtype=A.val.dtype))
     variants = [(pol, bind, th) for pol, bind in ((None, True), ("active", True), (None, False))
                 for th in a.threads]
+    Path(a.out).parent.mkdir(parents=True, exist_ok=True)
     with open(a.out, "w") as f:
         for rep in range(a.reps):
             for pol, bind, th in variants:
@@ -50,7 +51,9 @@ def main():
                 env["OMP_SCHEDULE"] = "static"
                 if pol:
                     env["OMP_WAIT_POLICY"] = pol
+                dump = Path(a.out).with_suffix("").as_posix() + f"_r{rep}_{pol or 'default'}_{'b' if bind else 'u'}{th}.npy"
                 cmd = [sys.executable, str(REPO / "oracle" / "cpu_bench.py"), "--dir", str(d),
+                       "--dump-samples", dump,
                        "--budget", str(a.budget), "--no-tried", "--threads", str(th)] + ([] if bind else ["--no-bind"])
                 out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
                 r = json.loads(out.stdout.strip().splitlines()[-1]) if out.returncode == 0 else {}

@@ -153,7 +153,7 @@ def reference_leg(rp, ci, val32, x32, nnz: int, threads: int, budget_s: float):
 
 
 def run(d: Path, budget_s: float, threads: int = 0, bind: bool = True, tried: bool = True,
-        reference: bool = True) -> dict:
+        reference: bool = True, dump: str = "") -> dict:
     rp = np.load(d / "row_ptr.npy", mmap_mode="r")
     ci = np.load(d / "col_idx.npy", mmap_mode="r")
     val = np.load(d / "val.npy", mmap_mode="r")
@@ -186,6 +186,8 @@ def run(d: Path, budget_s: float, threads: int = 0, bind: bool = True, tried: bo
         oracle.set_schedule(sched, threads)
         c0 = cpu_stat()
         smp = oracle.time_spmv_samples(lrp, lci, lval, x, 5, runs)
+        if dump and sched == "static":  # every run's seconds, in order (A/B diagnosis)
+            np.save(dump, smp)
         res[sched] = timing(nnz, smp)
         res[sched]["cgroup_throttling"] = throttled(c0, cpu_stat())
         # share of runs within 10 % / 50 % of TimeMin
@@ -234,8 +236,10 @@ def main():
     ap.add_argument("--no-bind", action="store_true")
     ap.add_argument("--no-tried", action="store_true")
     ap.add_argument("--no-reference", action="store_true")
+    ap.add_argument("--dump-samples", default="", help=".npy of the static leg's run times")
     a = ap.parse_args()
-    out = run(Path(a.dir), a.budget, a.threads, not a.no_bind, not a.no_tried, not a.no_reference)
+    out = run(Path(a.dir), a.budget, a.threads, not a.no_bind, not a.no_tried, not a.no_reference,
+              a.dump_samples)
     print(json.dumps(out), flush=True)
 
 
