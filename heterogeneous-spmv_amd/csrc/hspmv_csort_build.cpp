@@ -40,11 +40,11 @@ constexpr double kSweepPerRowBlock = 0.13;  // a column's sweep cost, in entries
 // paired blocks: largest part share of a block / the part's mean (C5's
 // power-law rows split over the parts unevenly enough for 1.047 at best)
 constexpr double kPairSlack = 1.06;
-// Row-partition weight of a crowded row's entries (ones that land >= 8 to a
-// chunk, so their chunks are segmented): a segmented chunk cost 0.164 us on
-// top of a plain one's ~0.37 us in the per-workgroup fit of c5r (entries,
-// gather quad-sectors, segmented chunks; r^2 0.92, r04a).
-constexpr int32_t kWUnit = 16, kWCrowded = 23;
+// Row-partition weight of crowded entries (>= 8 of one row to a chunk, so
+// their chunks are segmented): c5r's hub blocks ran 96-104 us against a
+// part median of 85 with the same entries and 100-160 segmented chunks
+// (profiles/r04/csort_trace_wg_cost_balanced.jsonl): ~1.6x per entry.
+constexpr int32_t kWUnit = 16, kWCrowded = 26;
 
 struct CsEnt {
   uint32_t col, slot, k;
@@ -170,49 +170,61 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   if (row_cap < 64) return HSPMV_OK;  // too many slices for the LDS: not this path
   // [h][r]: row r's in-kernel nonzeros in part h, then its partition weight
   std::vector<int32_t> cnt((size_t)(H * m), 0);
-  std::vector<int32_t> cmin((size_t)(H * m), INT32_MAX), cmax((size_t)(H * m), -1);
   std::vector<int64_t> tot_part((size_t)H, 0);
   const int ntc = (int)std::max<int64_t>(1, std::min<int64_t>(16, m / 65536));
   auto par_rows = [&](auto &&body) {
     std::vector<std::thread> th;
-    for (int t = 0; t < ntc; ++t) th.emplace_back([&, t]() { body(m * t / ntc, m * (t + 1) / ntc); });
+    for (int t = 0; t < ntc; ++t) th.emplace_back([&, t]() { body(t, m * t / ntc, m * (t + 1) / ntc); });
     for (auto &x : th) x.join();
   };
-  par_rows([&](int64_t r0, int64_t r1) {
+  par_rows([&](int, int64_t r0, int64_t r1) {
     for (int64_t r = r0; r < r1; ++r) {
       if (rp[r + 1] - rp[r] > long_t) continue;
-      for (int32_t k = rp[r]; k < rp[r + 1]; ++k) {
-        const size_t i = (size_t)(part_of(col[k]) * m + r);
-        ++cnt[i];
-        cmin[i] = std::min(cmin[i], col[k]);
-        cmax[i] = std::max(cmax[i], col[k]);
-      }
+      for (int32_t k = rp[r]; k < rp[r + 1]; ++k) ++cnt[(size_t)(part_of(col[k]) * m + r)];
     }
   });
   for (int h = 0; h < H; ++h)
     for (int64_t r = 0; r < m; ++r) tot_part[(size_t)h] += cnt[(size_t)(h * m + r)];
-  {
-    // crowded rows: entries per chunk ~ k * min(1, chunk span / row span),
-    // chunk span = the columns one chunk of a block covers
+  if (tn.csort_balance >= 0) {
+    // Crowded entries: ones with >= kCsortSegHeavy entries of the same row
+    // within the columns one chunk of a block covers (cspan) -- the entries
+    // that make their chunks segmented.  An RCM ordering clusters a hub
+    // row's columns, so the row's whole span says little: each entry's own
+    // window is counted (sorted copy of the row's part, two pointers).
     std::vector<double> cspan((size_t)H, 0.0);
     for (int h = 0; h < H; ++h)
       cspan[(size_t)h] = tot_part[(size_t)h] ? (double)C * (double)(pb[(size_t)h + 1] - pb[(size_t)h]) *
                                                    (double)nb0 / (double)tot_part[(size_t)h]
                                              : 0.0;
-    const bool weigh = tn.csort_balance >= 0;
-    par_rows([&](int64_t r0, int64_t r1) {
-      for (int h = 0; h < H; ++h)
-        for (int64_t r = r0; r < r1; ++r) {
-          const size_t i = (size_t)(h * m + r);
-          const int32_t k = cnt[i];
-          double per_chunk = 0.0;
-          if (k > 0) per_chunk = (double)k * std::min(1.0, cspan[(size_t)h] / (double)(cmax[i] - cmin[i] + 1));
-          cnt[i] = k * (weigh && per_chunk >= (double)kCsortSegHeavy ? kWCrowded : kWUnit);
+    par_rows([&](int, int64_t r0, int64_t r1) {
+      std::vector<int32_t> cs;
+      std::vector<int32_t> crowded((size_t)H);
+      for (int64_t r = r0; r < r1; ++r) {
+        const int32_t len = rp[r + 1] - rp[r];
+        if (len > long_t || len < kCsortSegHeavy) {
+          for (int h = 0; h < H; ++h) cnt[(size_t)(h * m + r)] *= kWUnit;
+          continue;
         }
+        cs.assign(col + rp[r], col + rp[r + 1]);
+        std::sort(cs.begin(), cs.end());
+        std::fill(crowded.begin(), crowded.end(), 0);
+        for (size_t i = 0, j = 0; i < cs.size(); ++i) {  // entries i..j-1 within cspan of cs[i]
+          const int h = part_of(cs[i]);
+          const double lim = (double)cs[i] + cspan[(size_t)h];
+          if (j < i + 1) j = i + 1;
+          while (j < cs.size() && (double)cs[j] < lim && part_of(cs[j]) == h) ++j;
+          if ((int64_t)(j - i) >= kCsortSegHeavy) ++crowded[(size_t)h];
+        }
+        for (int h = 0; h < H; ++h) {
+          const size_t i = (size_t)(h * m + r);
+          const int32_t cr = std::min(cnt[i], crowded[(size_t)h]);
+          cnt[i] = (cnt[i] - cr) * kWUnit + cr * kWCrowded;
+        }
+      }
     });
+  } else {
+    for (auto &v : cnt) v *= kWUnit;
   }
-  std::vector<int32_t>().swap(cmin);
-  std::vector<int32_t>().swap(cmax);
   // Greedy cuts at `target` weight or row_cap rows; the target is the
   // smallest that yields at most nb0 blocks (one block more would run a
   // second round of workgroups on one CU and double the launch).
