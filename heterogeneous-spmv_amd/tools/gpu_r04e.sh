@@ -10,5 +10,5 @@ step() {  # step NAME SECONDS CMD...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stop: $name rc=$rc"; exit $rc; fi
 }
 step csort_tests 300 python -u -m pytest tests/test_csort.py tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "csort or c5"
-step ab_pair 400 python $T/ab.py --libs "$E#HSPMV_CSORT_PAIR=-1,$E,$E#HSPMV_CSORT_PAIR=-1,$E" --configs c5 --rounds 9 --out $O/ab_c5_pair.jsonl
-step trace 240 python $T/csort_trace.py --configs c5 --per-wg --out $O/csort_trace_wg_paired.jsonl
+step ab_pair 400 python $T/ab.py --libs "$E#HSPMV_CSORT_PAIR=-1,$E,$E#HSPMV_CSORT_PAIR=-1,$E" --configs c5,c5r --rounds 7 --out $O/ab_c5_pair.jsonl
+step trace 240 python $T/csort_trace.py --configs c5,c5r --per-wg --out $O/csort_trace_wg_paired.jsonl
