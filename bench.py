@@ -582,8 +582,7 @@ def main():
         launches = 1 if csort else (info["x_slabs"] or 1)
         # csort: the finishing pass (column parts / long-row slices) unless the
         # block sums are written to y directly (one part, no long rows)
-        extra = (0 if ((info["csort_parts"] == 1 and not info["n_split_rows"]) or info["csort_paired"])
-                 else 1) if csort else \
+        extra = (0 if (info["csort_parts"] == 1 and not info["n_split_rows"]) else 1) if csort else \
             (2 if info["n_split_rows"] else 0)
         out = {
             "metric": METRIC,

@@ -169,9 +169,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     const int32_t *__restrict__ vslice, const int32_t *__restrict__ cbase,
     const void *__restrict__ ent, const T *__restrict__ val, const T *__restrict__ x,
     S *__restrict__ part, S *__restrict__ spart, T *__restrict__ y,
-    unsigned long long *__restrict__ trace, uint32_t *__restrict__ pair, int32_t row_blocks,
-    const int32_t *__restrict__ slice_row, const int32_t *__restrict__ long_row,
-    const int32_t *__restrict__ long_cs, const uint32_t *__restrict__ long_mask) {
+    unsigned long long *__restrict__ trace) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   S *acc = reinterpret_cast<S *>(smem);
   constexpr int NW = kCsortThreads / kWave;
@@ -285,81 +283,6 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     return;
   }
   S *out = part + (int64_t)h * m + r0;
-  if (pair) {
-    // Paired row blocks (H == 2, both parts' workgroups on the same rows,
-    // on different XCDs): the first to get here publishes its sums, the
-    // second adds them to its own -- part 0's + part 1's, in that order --
-    // and writes y.  Cross-XCD visibility without flushing either L2: the
-    // sums are stored and loaded as agent-scope atomics (sc1: coherent at
-    // the device level), the publisher waits for every store's
-    // acknowledgement (s_waitcnt vmcnt(0)) before raising the flag, and the
-    // second workgroup reads them only after seeing it.  The second spins
-    // only on a workgroup that has already finished its entries (it took
-    // the first arrival), so the wait is bounded by one slice write-out.
-    // The second resets both words for the next SpMV.
-    // Long-row slices first: every workgroup publishes its slices' sums
-    // (agent-scope stores, acknowledged), then counts them in per long row;
-    // the one that counts a row's last slice adds all of that row's slices
-    // in slice order and writes its y.  No waiting: a row's other slices are
-    // published before they are counted.
-    if (nv > 0) {
-      for (int32_t i = threadIdx.x; i < nv; i += kCsortThreads)
-        __hip_atomic_store(spart + vslice[v0 + i], acc[nr + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
-      uint32_t *lcnt = pair + 2 * row_blocks;
-      for (int32_t i = threadIdx.x; i < nv; i += kCsortThreads) {
-        const int32_t j = slice_row[vslice[v0 + i]];
-        const uint32_t ns = (uint32_t)(long_cs[j + 1] - long_cs[j]);
-        if (__hip_atomic_fetch_add(lcnt + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ns - 1u) {
-          S t = S(0);
-          for (int32_t k = long_cs[j]; k < long_cs[j + 1]; ++k)
-            t += __hip_atomic_load(spart + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          y[long_row[j]] = (T)t;
-          __hip_atomic_store(lcnt + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-    __shared__ uint32_t order;
-    const int32_t blk = b / 2;
-    uint32_t *arrive = pair + blk, *ready = pair + row_blocks + blk;
-    if (threadIdx.x == 0)
-      order = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (order == 0u) {
-      for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads)
-        __hip_atomic_store(out + i, acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // every wave waits for its own stores' acknowledgements (a barrier
-      // does not; neither does a workgroup-scope release fence on gfx950)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_store(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    if (threadIdx.x == 0) {
-      // bounded (200 ms of the 100 MHz s_memrealtime clock): a partner that
-      // never publishes -- counters left behind by an aborted launch -- must
-      // cost a wrong y on that block, never a hung launch; the reset below
-      // then repairs the counters for the next SpMV
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
-             __builtin_amdgcn_s_memrealtime() - t0 < 20000000ull)
-        __builtin_amdgcn_s_sleep(2);
-      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ready, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    const S *other = part + (int64_t)(1 - h) * m + r0;
-    for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) {
-      const int64_t r = r0 + i;
-      if (long_mask && ((long_mask[r >> 5] >> (r & 31)) & 1u)) continue;  // y from its slices
-      const S o = __hip_atomic_load(other + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      y[r] = (T)(h == 0 ? acc[i] + o : o + acc[i]);
-    }
-    return;
-  }
   for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) out[i] = acc[i];
   for (int32_t i = threadIdx.x; i < nv; i += kCsortThreads) spart[vslice[v0 + i]] = acc[nr + i];
 }
@@ -432,7 +355,7 @@ void launch_csort_main(const DevCsort &c, const T *x, S *part, S *spart, T *y, h
   hipLaunchKernelGGL((hspmv_csort<T, S, U, NT, PF, WIDE>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
                      (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
                      c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y,
-                     c.trace, c.pair, c.row_blocks, c.slice_row, c.long_row, c.long_cs, c.long_mask);
+                     c.trace);
 }
 
 template <typename T, typename S, int U, bool NT>
@@ -452,7 +375,7 @@ hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
     }
   }
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || c.direct || c.pair) return e;  // y written by the main kernel
+  if (e != hipSuccess || c.direct) return e;
   // rows per finishing thread: 4 (32-byte partial loads; C5 104.4 -> 103.5
   // us, c5r 110.0 -> 107.8 against 2, r04c/ab_c5_fin_rows.jsonl), fewer when
   // m is not a multiple; c.fin_rows overrides (A/B)

@@ -429,7 +429,6 @@ static int fill_info(hspmv_handle *h, hspmv_info *out) {
   out->csort_slot_bytes = s.plan.kernel == kCsort ? (s.dp.cs.slot32 ? 4 : 8) : 0;
   out->csort_row_blocks = s.plan.kernel == kCsort ? s.dp.cs.row_blocks : 0;
   out->rccl_version = h->rccl_version;
-  out->csort_paired = s.plan.kernel == kCsort && s.dp.cs.pair ? 1 : 0;
   for (auto &sh : h->shards)
     if (sh.plan.kernel == kCsort) {
       out->csort_chunks += sh.csort_chunks;

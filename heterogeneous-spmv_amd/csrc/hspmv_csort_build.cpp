@@ -37,9 +37,6 @@ constexpr int64_t kCsortSegExtra = 128;
 constexpr int64_t kCsortSegHeavy = 8;  // entries of one row in a chunk that make it a run
 constexpr double kPartSlack = 1.25;    // widest column part / (n / H) when balancing cost
 constexpr double kSweepPerRowBlock = 0.13;  // a column's sweep cost, in entries, per row block
-// paired blocks: largest part share of a block / the part's mean (C5's
-// power-law rows split over the parts unevenly enough for 1.047 at best)
-constexpr double kPairSlack = 1.06;
 // Row-partition weight of crowded entries (>= 8 of one row to a chunk, so
 // their chunks are segmented): c5r's hub blocks ran 96-104 us against a
 // part median of 85 with the same entries and 100-160 segmented chunks
@@ -89,13 +86,6 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX
                          : (s.tune.csort_long > 0 ? s.tune.csort_long : kLongRow);
   const int64_t nb0 = std::max<int64_t>(1, (int64_t)cus * bpc / H);
-  // Paired row blocks (Tuning.csort_pair >= 0, the default): with two column
-  // parts sharing ONE row partition, the two workgroups of a row block
-  // combine their sums in the launch -- the second to finish adds the first's
-  // published partial sums and writes y -- and each long row's slices are
-  // added by the workgroup that publishes its last slice (csort.hip), so
-  // there is no finishing launch.
-  const bool pair_try = H == 2 && tn.csort_pair >= 0;
   // Column parts: [pb[h], pb[h+1]).  Equal widths, or (Tuning.csort_balance
   // >= 0, the default) boundaries at equal shares of the parts' COST, each
   // part's width kept within kPartSlack of n / H.  A workgroup's time is
@@ -258,36 +248,9 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     cut_w(c, lo, &out);
   };
   std::vector<std::vector<int32_t>> brh((size_t)H);
-  bool paired = false;
-  if (pair_try) {
-    // one partition on the summed weights, kept when every block's share of
-    // each part is within kPairSlack of that part's mean (random columns:
-    // the parts split every row evenly; an RCM ordering does not)
-    std::vector<int32_t> wsum((size_t)m);
-    for (int64_t r = 0; r < m; ++r) wsum[(size_t)r] = cnt[(size_t)r] + cnt[(size_t)(m + r)];
-    std::vector<int32_t> cuts;
-    partition(wsum.data(), cuts);
-    const int64_t nbk = (int64_t)cuts.size() - 1;
-    double worst = 0.0;
-    for (int h = 0; h < H; ++h) {
-      int64_t tot_h = 0;
-      for (int64_t r = 0; r < m; ++r) tot_h += cnt[(size_t)(h * m + r)];
-      const double mean = (double)tot_h / (double)nbk;
-      for (int64_t b = 0; b < nbk; ++b) {
-        int64_t w = 0;
-        for (int32_t r = cuts[(size_t)b]; r < cuts[(size_t)b + 1]; ++r) w += cnt[(size_t)(h * m + r)];
-        worst = std::max(worst, mean > 0 ? (double)w / mean : 0.0);
-      }
-    }
-    if (worst <= kPairSlack) {
-      paired = true;
-      brh[0] = cuts;
-      brh[1] = cuts;
-    }
-  }
   int64_t NB = 0;
   for (int h = 0; h < H; ++h) {
-    if (!paired) partition(cnt.data() + (size_t)h * (size_t)m, brh[(size_t)h]);
+    partition(cnt.data() + (size_t)h * (size_t)m, brh[(size_t)h]);
     NB = std::max<int64_t>(NB, (int64_t)brh[(size_t)h].size() - 1);
   }
   std::vector<int32_t>().swap(cnt);
@@ -543,19 +506,6 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     s.d_cs_val = dv;
   }
   const bool direct = H == 1 && lrow.empty();
-  if (paired) {
-    // per row block an arrival count and the first arriver's "published"
-    // flag; per long row a count of its published slices; per slice its
-    // long row
-    std::vector<uint32_t> z((size_t)(2 * NB + (int64_t)lrow.size()), 0u);
-    if ((rc = up(&s.d_cs_pair, z))) return rc;
-    if (n_slices) {
-      std::vector<int32_t> srow((size_t)n_slices);
-      for (size_t j = 0; j + 1 < lcs.size(); ++j)
-        for (int32_t v = lcs[j]; v < lcs[j + 1]; ++v) srow[(size_t)v] = (int32_t)j;
-      if ((rc = up(&s.d_cs_slice_row, srow))) return rc;
-    }
-  }
   if (!direct) {  // partial sums in the slot type
     if ((rc = dev_alloc(&s.d_cs_part, slot_bytes * (size_t)H * (size_t)m, &s.bytes))) return rc;
     if ((rc = dev_alloc(&s.d_cs_spart, slot_bytes * (size_t)std::max<int64_t>(n_slices, 1), &s.bytes)))
@@ -574,8 +524,6 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.H = H;
   c.u = U;
   c.direct = direct ? 1 : 0;
-  c.pair = paired ? s.d_cs_pair : nullptr;
-  c.slice_row = paired ? s.d_cs_slice_row : nullptr;
   c.n_long = (int32_t)lrow.size();
   c.nontemporal = true;  // the entry stream is read once; keep x in the caches
   if (tn.csort_nt >= 0) c.nontemporal = tn.csort_nt != 0;  // A/B knobs
@@ -613,10 +561,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   // bytes moved: the entry stream + chunk bases + x (distinct columns) + the
   // partial sums written and read back + y
   const double xb = (double)s.x_entries * (double)sv;
-  // (paired: both workgroups of a block publish, the second reads one)
-  const double part_traffic = direct ? 0.0
-                              : paired ? 3.0 * (double)slot_bytes * (double)m
-                                       : 2.0 * (double)slot_bytes * ((double)H * (double)m + (double)n_slices);
+  const double part_traffic =
+      direct ? 0.0 : 2.0 * (double)slot_bytes * ((double)H * (double)m + (double)n_slices);
   s.csort_format_bytes = (double)tot * (double)(4 + sv) + 4.0 * (double)tot_chunks + xb + part_traffic +
                          (double)sv * (double)m;
   s.A.has_csort = true;

@@ -73,7 +73,6 @@ struct Tuning {
   int csort_long = 0;                    // rows above this many nonzeros are sliced (0: kLongRow)
   int csort_balance = 0;                 // -1: equal-width column parts, nnz-balanced rows (r03)
   int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4)
-  int csort_pair = 0;                    // -1: never pair the two column parts' row blocks
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
 };
@@ -114,11 +113,6 @@ struct DevCsort {
   void *part = nullptr, *spart = nullptr;  // partial sums in the slot type
   const uint32_t *long_mask = nullptr;
   const int32_t *long_row = nullptr, *long_cs = nullptr;
-  // paired row blocks (H == 2, one row partition): per block an arrival
-  // count and a published flag, per long row a count of published slices
-  // [2 * row_blocks + n_long]; slice_row: the long row of every slice
-  uint32_t *pair = nullptr;
-  const int32_t *slice_row = nullptr;
 };
 
 // Device-side tables the host planner builds once per shard (all optional).

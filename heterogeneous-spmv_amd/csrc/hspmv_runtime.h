@@ -63,11 +63,10 @@ struct Shard {
   int32_t n_slabs = 0;
   // column-sorted row blocks (build_csort): owned tables, and the launch
   // description they form (copied into dp.cs when the planner picks kCsort)
-  int32_t *d_cs_slice_row = nullptr;  // paired blocks: the long row of every slice
   int32_t *d_cs_blk_c = nullptr, *d_cs_blk_r = nullptr, *d_cs_blk_v = nullptr,
           *d_cs_vslice = nullptr, *d_cs_cbase = nullptr, *d_cs_long_row = nullptr,
           *d_cs_long_cs = nullptr;
-  uint32_t *d_cs_mask = nullptr, *d_cs_pair = nullptr;
+  uint32_t *d_cs_mask = nullptr;
   unsigned long long *d_cs_trace = nullptr;  // diagnostic builds: csort per-workgroup timestamps
   void *d_cs_ent = nullptr, *d_cs_val = nullptr;
   double *d_cs_part = nullptr, *d_cs_spart = nullptr;

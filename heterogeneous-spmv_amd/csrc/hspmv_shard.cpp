@@ -55,7 +55,7 @@ void free_shard(Shard &s, bool borrowed) {
   (void)hipFree(s.d_slab_val);
   for (void *p : {(void *)s.d_cs_blk_c, (void *)s.d_cs_blk_r, (void *)s.d_cs_blk_v,
                   (void *)s.d_cs_vslice, (void *)s.d_cs_cbase, (void *)s.d_cs_long_row,
-                  (void *)s.d_cs_long_cs, (void *)s.d_cs_mask, (void *)s.d_cs_pair, (void *)s.d_cs_slice_row, s.d_cs_ent, s.d_cs_val,
+                  (void *)s.d_cs_long_cs, (void *)s.d_cs_mask, s.d_cs_ent, s.d_cs_val,
                   (void *)s.d_cs_part, (void *)s.d_cs_spart, (void *)s.d_cs_trace})
     (void)hipFree(p);
   (void)hipFree(s.d_task);

@@ -117,7 +117,7 @@ class Info(C.Structure):
                 ("placement_us", C.c_double * 8),
                 ("deterministic", C.c_int32), ("csr3_plan", C.c_int32),
                 ("csort_slot_bytes", C.c_int32), ("csort_row_blocks", C.c_int32),
-                ("rccl_version", C.c_int32), ("csort_paired", C.c_int32),
+                ("rccl_version", C.c_int32), ("reserved0", C.c_int32),
                 ("csort_chunks", C.c_int64), ("csort_seg_chunks", C.c_int64)]
 
 

@@ -168,9 +168,7 @@ typedef struct {
                                resolved (librccl.so.1 is one SONAME for the
                                ROCm and the PyTorch copy: the first loaded
                                wins), e.g. 22703 = 2.27.3                   */
-  int32_t csort_paired;     /* CSORT: 1 = the two column parts share one row
-                               partition and combine their sums in the
-                               launch (no finishing pass); 0 otherwise     */
+  int32_t reserved0;
   int64_t csort_chunks;     /* CSORT: 64*U-entry chunks of the launch       */
   int64_t csort_seg_chunks; /* CSORT: of those, chunks stored slot-sorted
                                (crowded rows summed by a segmented scan)   */

@@ -210,9 +210,8 @@ def test_csort_segmented_chunks_for_contiguous_hub_rows(dtype):
 
 
 def _uniform_with_long_rows(dtype, seed=13, m=600_000, n=1_500_000):
-    """Short rows over random columns (every row splits evenly over the two
-    column parts, so the parts share one row partition: paired blocks) plus
-    long rows cut into slices, first / last / adjacent rows among them."""
+    """Short rows over random columns plus long rows cut into slices,
+    first / last / adjacent rows among them."""
     rng = np.random.default_rng(seed)
     lens = rng.integers(2, 16, m)
     for r, ln in [(0, 9000), (1, 4097), (777, 30_000), (778, 5000), (m - 1, 12_000)]:
@@ -225,25 +224,22 @@ def _uniform_with_long_rows(dtype, seed=13, m=600_000, n=1_500_000):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_csort_paired_blocks_and_slice_combine(dtype):
-    """Paired row blocks: the two column parts' workgroups of a row block
-    combine in the launch (the second adds the first's published sums), and
-    a long row's slices are added by the workgroup that publishes the last
-    one -- no finishing pass.  Every SpMV of a back-to-back run is checked
-    (which workgroup arrives second changes from launch to launch), and the
-    counters reset themselves between launches."""
+def test_csort_long_row_slices_repeated_launches(dtype):
+    """Short rows over random columns plus long rows cut into slices (first,
+    last, adjacent rows among them): every SpMV of a back-to-back run is
+    checked (the LDS atomic order changes from launch to launch), then a new
+    x (nothing stale from the last launch)."""
     A = _uniform_with_long_rows(dtype)
     x = gen.rand_x(A.n, 21).astype(dtype)
     lens = np.diff(A.row_ptr)
     with hspmv.SpMV(A, kernel="csort") as op:
         info = op.info
-        assert info["csort_parts"] == 2 and info["csort_paired"] == 1, info
-        assert info["n_split_rows"] == int((lens > 4096).sum())
+        assert info["csort_parts"] == 2 and info["n_split_rows"] == int((lens > 4096).sum())
         op.set_x(x)
         for _ in range(10):
             op.spmv()
             check(A, x, op.get_y())
-        x2 = gen.rand_x(A.n, 22).astype(dtype)  # a new x: nothing stale from the last launch
+        x2 = gen.rand_x(A.n, 22).astype(dtype)
         op.set_x(x2)
         op.spmv()
         check(A, x2, op.get_y())

@@ -337,14 +337,12 @@ def test_config_c5_powerlaw_csr3_fp32():
     y, info = gpu_spmv(A, x, maps)
     lens = np.diff(A.row_ptr)
     assert info["kernel_name"] == "csort" and info["csort_parts"] == 2
-    # random columns: both column parts share one row partition and their
-    # workgroups combine in the launch (paired, no finishing pass)
-    assert info["csort_paired"] == 1 and info["n_split_rows"] == int((lens > 4096).sum())
+    assert info["n_split_rows"] == int((lens > 4096).sum())
     y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
     absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
     y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
-    # every SpMV of a back-to-back run (the pairing's publish / read order
-    # varies from launch to launch)
+    # every SpMV of a back-to-back run (the LDS atomic order varies from
+    # launch to launch)
     with hspmv.SpMV(A, maps, device=0) as op:
         op.set_x(x)
         for it in range(12):
