@@ -50,67 +50,6 @@ struct CsEnt {
   }
 };
 
-// Quad packing of one gather instruction (64 lanes; o[0..63] = entries of
-// src, -1 = padding, which gathers x[base]).  The L1 serves an instruction
-// quad by quad (4 lanes) and returns one 32-byte sector per access, so the
-// gather's cost is the number of distinct (quad, sector) pairs, not of
-// sectors: in column order a sector's 1-3 entries straddle a quad boundary
-// often enough that C5's instructions cost ~41 accesses against ~34
-// distinct sectors (CPU model of C5's density).  The entries are regrouped
-// by sector, largest groups first, each into the first quad with room for
-// all of it (else split over the quads with room): the same gathers and
-// products, lanes permuted.
-static void pack_quads(const CsEnt *src, int32_t *o, uint32_t pad_sector, int shift) {
-  struct Grp { uint32_t sec; int n; int first; };
-  int32_t e[64];
-  uint32_t sc[64];
-  for (int q = 0; q < 64; ++q) {
-    e[q] = o[q];
-    sc[q] = o[q] >= 0 ? src[o[q]].col >> shift : pad_sector;
-  }
-  // entries in column order: a sector's entries are consecutive (padding last,
-  // its sector may repeat the chunk's first one: merged by the scan below)
-  Grp g[64];
-  int ng = 0;
-  int idx[64];
-  for (int q = 0; q < 64; ++q) idx[q] = q;
-  std::stable_sort(idx, idx + 64, [&](int a, int b) { return sc[a] < sc[b]; });
-  for (int q = 0; q < 64;) {
-    int r = q;
-    while (r < 64 && sc[idx[r]] == sc[idx[q]]) ++r;
-    g[ng++] = {sc[idx[q]], r - q, q};
-    q = r;
-  }
-  std::stable_sort(g, g + ng, [](const Grp &a, const Grp &b) { return a.n > b.n; });
-  int cap[16], fill[16];
-  for (int k = 0; k < 16; ++k) {
-    cap[k] = 4;
-    fill[k] = 0;
-  }
-  int32_t out[64];
-  auto put = [&](int k, int from, int cnt) {
-    for (int t = 0; t < cnt; ++t) out[4 * k + fill[k] + t] = e[idx[from + t]];
-    fill[k] += cnt;
-    cap[k] -= cnt;
-  };
-  for (int a = 0; a < ng; ++a) {
-    int left = g[a].n, from = g[a].first;
-    for (int k = 0; k < 16 && left > 0; ++k)
-      if (cap[k] >= left) {
-        put(k, from, left);
-        left = 0;
-      }
-    for (int k = 0; k < 16 && left > 0; ++k)
-      if (cap[k] > 0) {
-        const int c = std::min(cap[k], left);
-        put(k, from, c);
-        from += c;
-        left -= c;
-      }
-  }
-  for (int q = 0; q < 64; ++q) o[q] = out[q];
-}
-
 int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
                 int64_t n, int dtype, unsigned flags) {
   if (m == 0 || n == 0 || !val) return HSPMV_OK;
@@ -435,7 +374,6 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
             return (u / per) * (64 * per) + lane * per + (u % per);
           };
           std::vector<CsEnt> tmp;
-          std::vector<int32_t> ord((size_t)C);
           uint32_t sl64[64];
           chunk_walk(E, [&](int64_t ci, uint32_t c0, int64_t i, int64_t j) {
             const int64_t ch = cfirst + ci;
@@ -491,16 +429,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
               }
             }
             cbase[(size_t)ch] = (int32_t)(c0 | (seg ? 0x80000000u : 0u));
-            // lane order: ord[q] = the entry (index into src) lane q % 64 of
-            // instruction q / 64 gathers for, -1 = padding (x[base]); column
-            // order, or (plain chunks, Tuning.csort_pack >= 0) each
-            // instruction's entries packed so that one x sector's entries
-            // share a quad (pack_quads)
-            const int64_t ne = j - i;
-            for (int64_t q = 0; q < C; ++q) ord[(size_t)q] = q < ne ? (int32_t)q : -1;
-            if (!seg && tn.csort_pack >= 0)
-              for (int64_t g = 0; g < C && g < ne; g += 64)
-                pack_quads(src, ord.data() + g, c0 >> sec_shift, sec_shift);
+            const int64_t ne = j - i;  // lanes >= ne: padding (gathers x[base])
             if (stats) {
               int64_t *w = wst.data() + kWgStats * b;
               w[2] += 1;
@@ -509,7 +438,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
               for (int64_t g = 0; g < C; g += 64) {  // one gather instruction
                 uint32_t sec[64];
                 for (int64_t q = 0; q < 64; ++q)
-                  sec[q] = (ord[(size_t)(g + q)] >= 0 ? src[ord[(size_t)(g + q)]].col : c0) >> sec_shift;
+                  sec[q] = (g + q < ne ? src[g + q].col : c0) >> sec_shift;
                 for (int64_t q = 0; q < 64; q += 4) {  // the L1 serves each quad on its own
                   int d = 1;
                   for (int t = 1; t < 4; ++t) {
@@ -528,8 +457,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
               const int64_t ov = ch * C + at(q, 2);
               uint32_t ix = dummy << 16;  // padding: 0 * x[base] into the dummy slot
               const void *vp = nullptr;
-              if (ord[(size_t)q] >= 0) {
-                const CsEnt &e = src[ord[(size_t)q]];
+              if (q < ne) {
+                const CsEnt &e = src[q];
                 ix = (e.slot << 16) | (e.col - c0);
                 vp = (const char *)val + sv * (size_t)e.k;
               }

@@ -73,7 +73,6 @@ struct Tuning {
   int csort_long = 0;                    // rows above this many nonzeros are sliced (0: kLongRow)
   int csort_balance = 0;                 // -1: equal-width column parts, nnz-balanced rows (r03)
   int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4)
-  int csort_pack = 0;                    // -1: gather lanes in column order (no quad packing)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
 };

@@ -83,7 +83,6 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_CSORT_LONG", &t->csort_long);
   geti("HSPMV_CSORT_BALANCE", &t->csort_balance);
   geti("HSPMV_CSORT_FIN_ROWS", &t->csort_fin_rows);
-  geti("HSPMV_CSORT_PACK", &t->csort_pack);
   geti("HSPMV_STREAM_W", &t->stream_waves);
   geti("HSPMV_PLACEMENT", &t->placement_trials);
   geti("HSPMV_CONTIG", &t->contig);
