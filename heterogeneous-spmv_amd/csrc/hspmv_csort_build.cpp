@@ -175,6 +175,11 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   });
   for (int h = 0; h < H; ++h)
     for (int64_t r = 0; r < m; ++r) tot_part[(size_t)h] += cnt[(size_t)(h * m + r)];
+  // a row's partition weight (int32: a row of > 2^31 / kWCrowded entries,
+  // possible only unsplit, saturates)
+  auto weigh = [](int64_t plain, int64_t crowded) {
+    return (int32_t)std::min<int64_t>(INT32_MAX / 2, plain * kWUnit + crowded * kWCrowded);
+  };
   if (tn.csort_balance >= 0) {
     // Crowded entries: ones with >= kCsortSegHeavy entries of the same row
     // within the columns one chunk of a block covers (cspan) -- the entries
@@ -192,7 +197,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
       for (int64_t r = r0; r < r1; ++r) {
         const int32_t len = rp[r + 1] - rp[r];
         if (len > long_t || len < kCsortSegHeavy) {
-          for (int h = 0; h < H; ++h) cnt[(size_t)(h * m + r)] *= kWUnit;
+          for (int h = 0; h < H; ++h) cnt[(size_t)(h * m + r)] = weigh(cnt[(size_t)(h * m + r)], 0);
           continue;
         }
         cs.assign(col + rp[r], col + rp[r + 1]);
@@ -208,12 +213,12 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
         for (int h = 0; h < H; ++h) {
           const size_t i = (size_t)(h * m + r);
           const int32_t cr = std::min(cnt[i], crowded[(size_t)h]);
-          cnt[i] = (cnt[i] - cr) * kWUnit + cr * kWCrowded;
+          cnt[i] = weigh(cnt[i] - cr, cr);
         }
       }
     });
   } else {
-    for (auto &v : cnt) v *= kWUnit;
+    for (auto &v : cnt) v = weigh(v, 0);
   }
   // Greedy cuts at `target` weight or row_cap rows; the target is the
   // smallest that yields at most nb0 blocks (one block more would run a
