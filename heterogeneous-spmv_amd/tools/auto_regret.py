@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""How far the AUTO planner lands from the best kernel, on matrices it was
+not fitted to.
+
+For each matrix of a zoo -- the BASELINE configurations plus shapes a user
+may bring (uniform random columns, dense diagonal blocks, an arrowhead,
+a wide x, a tall matrix over a tiny x, a diagonal, C5 in fp64) -- the AUTO
+handle and every forced kernel (stream, vector at two widths, csr3 over the
+maps or heavy tasks, csort) are timed in ONE process over the same device
+arrays (tools/sweep.py's DeviceMatrix, interleaved rounds, hspmv_run's
+per-launch events), each y checked against the oracle, and one JSON line per
+matrix reports AUTO's kernel and time, the fastest variant and
+regret = t_auto / t_best.
+
+    python heterogeneous-spmv_amd/tools/auto_regret.py [--zoo all|name,...]
+           [--rounds 3] [--iters 20] [--out profiles/rNN_auto_regret.jsonl]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parent.parent
+sys.path.insert(0, str(HERE))
+sys.path.insert(0, str(HERE.parent))
+sys.path.insert(0, str(REPO / "oracle"))
+
+import hspmv  # noqa: E402
+from hspmv import gen  # noqa: E402
+
+BASE = ["c2", "c3", "c3h", "c4", "c5", "c5r", "mix", "d24", "d64", "d512"]
+EXTRA = ["urand8", "urand32", "blocks32", "arrow", "wide", "tall", "diag", "c5d"]
+
+
+def _rows_random(m: int, n: int, k: int, seed: int, dtype=np.float64) -> hspmv.CsrMatrix:
+    """m rows of k uniform random columns in [0, n) (sorted; duplicates kept)."""
+    rng = np.random.default_rng(seed)
+    ci = np.sort(rng.integers(0, n, (m, k), dtype=np.int32), axis=1).reshape(-1)
+    rp = np.arange(0, m * k + 1, k, dtype=np.int64).astype(np.int32)
+    return hspmv.CsrMatrix(m, n, rp, ci, rng.uniform(-1, 1, m * k).astype(dtype))
+
+
+def build(name: str):
+    """(A, maps, description) of one zoo matrix."""
+    if name in BASE:
+        import sweep
+        return sweep.build(name)
+    if name == "urand8":
+        return _rows_random(4_000_000, 4_000_000, 8, 1), None, "uniform random columns, 4M x 4M, 8/row fp64"
+    if name == "urand32":
+        return _rows_random(1_500_000, 1_500_000, 32, 2), None, "uniform random columns, 1.5M x 1.5M, 32/row fp64"
+    if name == "blocks32":
+        m, b = 1_500_000, 32
+        rows = np.arange(m, dtype=np.int64)
+        ci = ((rows // b) * b)[:, None] + np.arange(b, dtype=np.int64)[None, :]
+        rng = np.random.default_rng(3)
+        rp = np.arange(0, m * b + 1, b, dtype=np.int64).astype(np.int32)
+        A = hspmv.CsrMatrix(m, m, rp, ci.reshape(-1).astype(np.int32), rng.uniform(-1, 1, m * b))
+        return A, None, "dense 32x32 diagonal blocks, 1.5M rows fp64"
+    if name == "arrow":
+        import scipy.sparse as sp
+        B = gen.banded(4_000_000, per_row=8, half=16, seed=4)
+        rng = np.random.default_rng(4)
+        heads = rng.choice(B.m, 16, replace=False)
+        hr = np.repeat(heads, 500_000)
+        hc = rng.integers(0, B.m, hr.shape[0])
+        S = sp.csr_matrix((B.val, B.col_idx, B.row_ptr), shape=(B.m, B.m)).tocoo()
+        r = np.concatenate([S.row, hr])
+        c = np.concatenate([S.col, hc])
+        v = np.concatenate([S.data, rng.uniform(-1, 1, hr.shape[0])])
+        T = sp.csr_matrix((v, (r, c)), shape=(B.m, B.m))
+        T.sum_duplicates()
+        return (hspmv.CsrMatrix.from_scipy(T, np.float64), None,
+                "arrowhead: banded 4M rows 8/row +-16 plus 16 rows of ~500K random columns fp64")
+    if name == "wide":
+        return _rows_random(250_000, 16_000_000, 128, 5), None, "wide: 250K x 16M, 128 random columns/row fp64"
+    if name == "tall":
+        return _rows_random(16_000_000, 4096, 3, 6), None, "tall: 16M x 4096, 3 random columns/row fp64"
+    if name == "diag":
+        m = 32_000_000
+        rp = np.arange(m + 1, dtype=np.int32)
+        return (hspmv.CsrMatrix(m, m, rp, np.arange(m, dtype=np.int32),
+                                np.random.default_rng(7).uniform(-1, 1, m)), None, "diagonal 32M fp64")
+    if name == "c5d":
+        import sweep
+        A, maps, desc = sweep.build("c5")
+        return A.astype(np.float64), maps, desc.replace("fp32", "fp64")
+    raise ValueError(name)
+
+
+def variants(A, maps):
+    d = A.nnz / max(A.m, 1)
+    v = [("auto", dict(kernel="auto"), maps)]
+    if maps is not None:
+        v.append(("auto-nomaps", dict(kernel="auto"), None))
+    v.append(("stream", dict(kernel="stream"), None))
+    for L in ((4, 8) if d < 16 else (16, 64)):
+        v.append((f"vector{L}", dict(kernel="vector", lanes=L), None))
+    v.append(("csr3", dict(kernel="csr3"), maps))
+    v.append(("csort", dict(kernel="csort"), None))
+    return v
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--zoo", default="all")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    import oracle
+    import sweep
+    names = BASE + EXTRA if a.zoo == "all" else a.zoo.split(",")
+    lines = []
+    for name in names:
+        t0 = time.time()
+        A, maps, desc = build(name)
+        x = gen.rand_x(A.n, 42).astype(A.val.dtype)
+        y_ref = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+        absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+        print(f"# {name}: {desc} m={A.m} n={A.n} nnz={A.nnz} built in {time.time() - t0:.1f}s",
+              file=sys.stderr, flush=True)
+        dev = sweep.DeviceMatrix(A, x)
+        ops = []
+        for vname, kw, mp in variants(A, maps):
+            try:
+                op = dev.spmv(mp, **kw)
+            except hspmv.HspmvError as e:  # e.g. csort refused for this shape
+                print(f"#   {vname}: not built ({e})", file=sys.stderr, flush=True)
+                continue
+            dev.y.fill_(float("nan"))
+            dev.torch.cuda.synchronize()
+            op.spmv()
+            op.synchronize()
+            y = dev.y.cpu().numpy().astype(np.float64)
+            f64 = A.val.dtype == np.float64
+            tol = (1e-6 if f64 else 1e-4) * np.abs(y_ref) + (1e-12 if f64 else 1e-5) * absrow
+            ok = bool(np.all(np.abs(y - y_ref) <= tol))
+            ops.append((vname, op, ok))
+        times = {v: [] for v, _, _ in ops}
+        for _ in range(a.rounds):
+            for vname, op, _ in ops:
+                times[vname].append(op.run(warmup=3, iters=a.iters)["t_min"])
+        res = {}
+        for vname, op, ok in ops:
+            res[vname] = {"t_us": round(min(times[vname]) * 1e6, 3), "kernel": op.info["kernel_name"],
+                          "ok": ok}
+            op.close()
+        timed = {k: v for k, v in res.items() if v["ok"]}
+        best = min(timed, key=lambda k: timed[k]["t_us"]) if timed else None
+        auto = res.get("auto")
+        rec = {"matrix": name, "desc": desc, "m": A.m, "n": A.n, "nnz": A.nnz,
+               "dtype": str(A.val.dtype), "maps": maps is not None,
+               "auto_kernel": auto["kernel"] if auto else None,
+               "auto_us": auto["t_us"] if auto else None,
+               "best": best, "best_us": timed[best]["t_us"] if best else None,
+               "regret": (round(auto["t_us"] / timed[best]["t_us"], 4) if auto and best else None),
+               "all_ok": all(v["ok"] for v in res.values()), "variants": res}
+        lines.append(rec)
+        print(json.dumps(rec), flush=True)
+        del dev
+    if a.out:
+        Path(a.out).write_text("".join(json.dumps(r) + "\n" for r in lines))
+
+
+if __name__ == "__main__":
+    main()

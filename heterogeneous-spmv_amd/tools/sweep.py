@@ -171,12 +171,6 @@ def variants(cfg, A, maps, full=False):
     v.append(("stream-auto-nt", dict(kernel="stream", nontemporal=True), None))
     v.append(("stream-auto-c32", dict(kernel="stream", col16=False), None))
     v.append((tag3 + "-auto-c32", dict(kernel="csr3", col16=False), m3))
-    if cfg in ("c3h", "c3hm"):  # DIMACS10 hugebubbles-00000 stand-in (degree-3 mesh, RCM)
-        A = gen.honeycomb(4280, 4280)
-        if cfg == "c3h":
-            return A, None, "C3 alt: honeycomb 4280^2 RCM (18.3M rows, 54.9M nnz) CSR fp64"
-        maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "volta"))
-        return A, maps, "C3 alt: honeycomb 4280^2 RCM CSR-3 fp64 (volta grouping)"
     if cfg == "c5":
         v.append(("stream-nosplit", dict(kernel="stream", split_rows=False), None))
     return v
