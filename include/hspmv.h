@@ -177,7 +177,10 @@ typedef struct {
 typedef struct hspmv_handle hspmv_handle;
 
 /* ---------------------------------------------------------------- flags */
-#define HSPMV_KERNEL_AUTO 0u   /* STREAM for CSR, CSR3 when maps given    */
+#define HSPMV_KERNEL_AUTO 0u   /* the planner's pick by shape: STREAM or
+                                  CSR3 tasks (CSR3 over maps when given),
+                                  CSORT for irregular gathers; the choice
+                                  is in hspmv_info.kernel                 */
 #define HSPMV_KERNEL_VECTOR 1u /* L lanes (sub-wave) per row, shuffle sum  */
 #define HSPMV_KERNEL_STREAM 2u /* wave per 64-row group, LDS-staged,
                                   ordered per-row sums (bit-exact vs CPU)  */
