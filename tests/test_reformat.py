@@ -92,3 +92,38 @@ def test_plain_reformat_and_overrides(tmp_path):
     run(BUILD / "reformat-auto", src, out3, "--ssrs", "5", "--srs", "3")
     B3, m3 = hspmv.read_csr3(out3, np.float64)
     assert np.array_equal(B3.col_idx, B.col_idx) and m3.inner[-1] == B3.m
+
+
+REF_STATS = REPO / "oracle" / "_ref" / "stats"
+
+
+@pytest.mark.parametrize("name", ["lap32.mtx.rcm", "powerlaw1500", "banded3000"])
+def test_csr_stats_matches_reference_tool(tmp_path, name):
+    """csr-stats prints what the reference's spmv-csr/stats.c prints (its
+    binary, built from the reference's sources by `make -C oracle ref`, is
+    the checker; fixtures without empty rows, where stats.c reads outside
+    the row)."""
+    if not REF_STATS.exists():
+        pytest.skip("oracle/_ref/stats not built (needs /root/reference)")
+    src = GOLDEN / f"{name}.csr"
+    ours = run(BUILD / "csr-stats", src).stdout
+    ref = run(REF_STATS, src).stdout
+    assert ours == ref
+    # the .csr3 form: the same statistics of its embedded CSR, plus the maps
+    A = hspmv.read_csr(src, np.float32)
+    out = tmp_path / "o.csr3"
+    run(BUILD / "reformat-auto", src, out)
+    B, maps = hspmv.read_csr3(out, np.float64)
+    s3 = run(BUILD / "csr-stats", out).stdout
+    assert f"Total NNZ: {A.nnz}\n" in s3 and f"Dim: {A.m}x{A.n}\n" in s3
+    assert f"Super-super-rows: {maps.n_ssr} Super-rows: {maps.n_sr}" in s3
+
+
+def test_csr_stats_empty_rows_and_usage():
+    p = run(BUILD / "csr-stats")
+    assert "inputfile" in p.stdout
+    s = run(BUILD / "csr-stats", GOLDEN / "empty_rows.csr").stdout
+    A = hspmv.read_csr(GOLDEN / "empty_rows.csr", np.float64)
+    lens = np.diff(A.row_ptr)
+    assert f"NNZ Min: {lens.min()}  " in s and f"NNZ Max: {lens.max()}  " in s
+    assert f"NNZ Var: {np.var(lens):f} " in s
