@@ -280,6 +280,45 @@ void uncoarsen(std::vector<int32_t> &map, const std::vector<int32_t> &perm_coars
   for (size_t i = 0; i < perm_finer.size(); ++i) perm_finer[i] = old_perm[(size_t)np[i]];
 }
 
+// reorderA (csrk.cu:722-870): new row i = row perm0[i] of A, columns
+// renumbered by the inverse permutation and sorted per row, values moved.
+int permute_symmetric(const hspmv_csr *A, const std::vector<int32_t> &perm0, hspmv_csr_buf *A_out) {
+  const int64_t m = A->m, nnz = A->nnz;
+  std::vector<int32_t> fwd((size_t)m);
+  for (int64_t i = 0; i < m; ++i) fwd[(size_t)perm0[(size_t)i]] = (int32_t)i;
+  const size_t sv = dtype_size(A->dtype);
+  A_out->m = m;
+  A_out->n = m;
+  A_out->nnz = nnz;
+  A_out->dtype = A->dtype;
+  A_out->row_ptr = (int32_t *)malloc(4 * (size_t)(m + 1));
+  A_out->col_idx = (int32_t *)malloc(4 * (size_t)(nnz ? nnz : 1));
+  A_out->val = malloc(sv * (size_t)(nnz ? nnz : 1));
+  if (!A_out->row_ptr || !A_out->col_idx || !A_out->val) {
+    hspmv_free_csr(A_out);
+    return set_error(HSPMV_E_NOMEM, "out of host memory");
+  }
+  A_out->row_ptr[0] = 0;
+  for (int64_t i = 0; i < m; ++i) {
+    const int32_t o = perm0[(size_t)i];
+    A_out->row_ptr[i + 1] = A_out->row_ptr[i] + (A->row_ptr[o + 1] - A->row_ptr[o]);
+  }
+  std::vector<std::pair<int32_t, int32_t>> row;
+  for (int64_t i = 0; i < m; ++i) {
+    const int32_t o = perm0[(size_t)i];
+    row.clear();
+    for (int32_t k = A->row_ptr[o]; k < A->row_ptr[o + 1]; ++k) row.push_back({fwd[(size_t)A->col_idx[k]], k});
+    std::sort(row.begin(), row.end());
+    int32_t at = A_out->row_ptr[i];
+    for (const auto &e : row) {
+      A_out->col_idx[at] = e.first;
+      memcpy((char *)A_out->val + sv * (size_t)at, (const char *)A->val + sv * (size_t)e.second, sv);
+      ++at;
+    }
+  }
+  return HSPMV_OK;
+}
+
 // levels = 3: CSR-3 (sizes s1 then s2, two coarsenings); levels = 2: CSR-2
 // (one coarsening with s1; the maps get an identity outer level, one
 // super-row per super-super-row).  BAND_k::preprocessingForSpMV's loop runs
@@ -327,43 +366,16 @@ int bandk_build(const hspmv_csr *A, int levels, int ssrs, int srs, hspmv_csr_buf
     if (levels == 3 && g2.n > 0) uncoarsen(map2, perm2, perm1);
     if (g1.n > 0) uncoarsen(map1, perm1, perm0);
     // reorderA: symmetric permutation, columns sorted per row
-    std::vector<int32_t> fwd((size_t)m);
-    for (int64_t i = 0; i < m; ++i) fwd[(size_t)perm0[(size_t)i]] = (int32_t)i;
-    const size_t sv = dtype_size(A->dtype);
-    A_out->m = m;
-    A_out->n = m;
-    A_out->nnz = nnz;
-    A_out->dtype = A->dtype;
-    A_out->row_ptr = (int32_t *)malloc(4 * (size_t)(m + 1));
-    A_out->col_idx = (int32_t *)malloc(4 * (size_t)(nnz ? nnz : 1));
-    A_out->val = malloc(sv * (size_t)(nnz ? nnz : 1));
+    rc = permute_symmetric(A, perm0, A_out);
+    if (rc) return rc;
     maps_out->n_ssr = g2.n;
     maps_out->n_sr = g1.n;
     maps_out->outer = (int32_t *)malloc(4 * (size_t)(g2.n + 1));
     maps_out->inner = (int32_t *)malloc(4 * (size_t)(g1.n + 1));
-    if (!A_out->row_ptr || !A_out->col_idx || !A_out->val || !maps_out->outer || !maps_out->inner) {
+    if (!maps_out->outer || !maps_out->inner) {
       hspmv_free_csr(A_out);
       hspmv_free_csr3(maps_out);
       return set_error(HSPMV_E_NOMEM, "out of host memory");
-    }
-    A_out->row_ptr[0] = 0;
-    for (int64_t i = 0; i < m; ++i) {
-      const int32_t o = perm0[(size_t)i];
-      A_out->row_ptr[i + 1] = A_out->row_ptr[i] + (A->row_ptr[o + 1] - A->row_ptr[o]);
-    }
-    std::vector<std::pair<int32_t, int32_t>> row;
-    for (int64_t i = 0; i < m; ++i) {
-      const int32_t o = perm0[(size_t)i];
-      row.clear();
-      for (int32_t k = A->row_ptr[o]; k < A->row_ptr[o + 1]; ++k)
-        row.push_back({fwd[(size_t)A->col_idx[k]], k});
-      std::sort(row.begin(), row.end());
-      int32_t at = A_out->row_ptr[i];
-      for (const auto &e : row) {
-        A_out->col_idx[at] = e.first;
-        memcpy((char *)A_out->val + sv * (size_t)at, (const char *)A->val + sv * (size_t)e.second, sv);
-        ++at;
-      }
     }
     memcpy(maps_out->outer, map2.data(), 4 * (size_t)(g2.n + 1));
     memcpy(maps_out->inner, map1.data(), 4 * (size_t)(g1.n + 1));
@@ -386,4 +398,90 @@ extern "C" int hspmv_build_csr3_bandk(const hspmv_csr *A, int ssrs, int srs, hsp
 extern "C" int hspmv_build_csr2_bandk(const hspmv_csr *A, int srs, hspmv_csr_buf *A_out,
                                       hspmv_csr3_buf *maps_out, int32_t *perm_out) {
   return bandk_build(A, 2, srs, 1, A_out, maps_out, perm_out);
+}
+
+// Reverse Cuthill-McKee of A's symmetrised pattern, the ordering the
+// reference's converter applies before writing its .rcm.csr inputs
+// (helpers/converter.m:14-15, Octave's symrcm).  Octave's implementation is
+// not restated (its tie-breaking is not pinned; Octave is absent here): per
+// connected component, BFS from a pseudo-peripheral vertex (the band-k
+// build's search, csrk.cu:2571-2669), unvisited neighbours in increasing
+// degree (then index), and the whole order reversed.  Outputs P A P^T with
+// sorted columns and, if perm != NULL, perm[m] (new row i = row perm[i]).
+extern "C" int hspmv_rcm_reorder(const hspmv_csr *A, hspmv_csr_buf *A_out, int32_t *perm_out) {
+  clear_error();
+  if (!A_out) return set_error(HSPMV_E_INVALID, "NULL output");
+  memset(A_out, 0, sizeof(*A_out));
+  int rc = validate_host_csr(A, true);
+  if (rc) return rc;
+  if (A->m != A->n) return set_error(HSPMV_E_INVALID, "RCM needs a square matrix (m = %lld, n = %lld)",
+                                     (long long)A->m, (long long)A->n);
+  const int64_t m = A->m;
+  try {
+    // the pattern of A + A^T without the diagonal
+    Graph g;
+    g.n = m;
+    std::vector<int64_t> cnt((size_t)m + 1, 0);
+    for (int64_t r = 0; r < m; ++r)
+      for (int32_t k = A->row_ptr[r]; k < A->row_ptr[r + 1]; ++k)
+        if (A->col_idx[k] != r) {
+          ++cnt[(size_t)r + 1];
+          ++cnt[(size_t)A->col_idx[k] + 1];
+        }
+    for (int64_t i = 0; i < m; ++i) cnt[(size_t)i + 1] += cnt[(size_t)i];
+    std::vector<int32_t> adj((size_t)cnt[(size_t)m]);
+    {
+      std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
+      for (int64_t r = 0; r < m; ++r)
+        for (int32_t k = A->row_ptr[r]; k < A->row_ptr[r + 1]; ++k)
+          if (A->col_idx[k] != r) {
+            adj[(size_t)fill[(size_t)r]++] = A->col_idx[k];
+            adj[(size_t)fill[(size_t)A->col_idx[k]]++] = (int32_t)r;
+          }
+    }
+    g.r.assign((size_t)m + 1, 0);
+    for (int64_t r = 0; r < m; ++r) {
+      auto b = adj.begin() + cnt[(size_t)r], e = adj.begin() + cnt[(size_t)r + 1];
+      std::sort(b, e);
+      g.c.insert(g.c.end(), b, std::unique(b, e));
+      g.r[(size_t)r + 1] = (int64_t)g.c.size();
+    }
+    std::vector<int32_t>().swap(adj);
+    g.deg.assign(g.c.size(), 1);
+    std::vector<int32_t> order;
+    order.reserve((size_t)m);
+    std::vector<int32_t> mask((size_t)m, 1), lr((size_t)m + 1), lc((size_t)m + 1), kids;
+    auto degree = [&](int32_t v) { return g.r[(size_t)v + 1] - g.r[(size_t)v]; };
+    for (int64_t s = 0; s < m; ++s) {
+      if (mask[(size_t)s] == 0) continue;
+      int32_t root = (int32_t)s;
+      pseudo_peripheral(root, g, mask, lr, lc);
+      size_t head = order.size();
+      order.push_back(root);
+      mask[(size_t)root] = 0;
+      while (head < order.size()) {
+        const int32_t v = order[head++];
+        kids.clear();
+        for (int64_t k = g.r[(size_t)v]; k < g.r[(size_t)v + 1]; ++k) {
+          const int32_t a = g.c[(size_t)k];
+          if (mask[(size_t)a]) {
+            mask[(size_t)a] = 0;
+            kids.push_back(a);
+          }
+        }
+        std::sort(kids.begin(), kids.end(), [&](int32_t a, int32_t b) {
+          return degree(a) != degree(b) ? degree(a) < degree(b) : a < b;
+        });
+        order.insert(order.end(), kids.begin(), kids.end());
+      }
+    }
+    std::reverse(order.begin(), order.end());
+    rc = permute_symmetric(A, order, A_out);
+    if (rc) return rc;
+    if (perm_out) memcpy(perm_out, order.data(), 4 * (size_t)m);
+  } catch (const std::bad_alloc &) {
+    hspmv_free_csr(A_out);
+    return set_error(HSPMV_E_NOMEM, "out of host memory");
+  }
+  return HSPMV_OK;
 }

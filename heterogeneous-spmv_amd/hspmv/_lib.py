@@ -189,6 +189,8 @@ SIGNATURES = {
     "hspmv_get_info_sized": (C.c_int, [_H, C.POINTER(Info), C.c_uint32]),
     "hspmv_destroy": (None, [_H]),
     "hspmv_read_csr": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(CsrBuf)]),
+    "hspmv_read_mtx": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(CsrBuf)]),
+    "hspmv_rcm_reorder": (C.c_int, [C.POINTER(Csr), C.POINTER(CsrBuf), C.c_void_p]),
     "hspmv_read_csr3": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(CsrBuf), C.POINTER(Csr3Buf)]),
     "hspmv_write_csr": (C.c_int, [C.c_char_p, C.POINTER(Csr)]),
     "hspmv_write_csr3": (C.c_int, [C.c_char_p, C.POINTER(Csr), C.POINTER(Csr3Maps)]),

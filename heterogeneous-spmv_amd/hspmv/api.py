@@ -154,6 +154,24 @@ def read_csr(path: str, dtype=np.float64) -> CsrMatrix:
     return _take_csr(buf)
 
 
+def read_mtx(path: str, dtype=np.float64) -> CsrMatrix:
+    """Matrix Market coordinate file as mmread.m + sparse2csr.m read it
+    (hspmv_read_mtx: symmetric files expanded, duplicates summed, zeros
+    dropped, columns sorted)."""
+    buf = _lib.CsrBuf()
+    check(lib().hspmv_read_mtx(str(path).encode(), dtype_code(dtype), C.byref(buf)), "read_mtx")
+    return _take_csr(buf)
+
+
+def rcm_reorder(A: CsrMatrix):
+    """Reverse Cuthill-McKee of A's symmetrised pattern (hspmv_rcm_reorder):
+    (A_perm, perm) with row i of A_perm = row perm[i] of A."""
+    cs, buf = A.c_struct(), _lib.CsrBuf()
+    perm = np.empty(A.m, np.int32)
+    check(lib().hspmv_rcm_reorder(C.byref(cs), C.byref(buf), _ptr(perm)), "rcm_reorder")
+    return _take_csr(buf), perm
+
+
 def read_csr3(path: str, dtype=np.float64):
     buf, mbuf = _lib.CsrBuf(), _lib.Csr3Buf()
     check(lib().hspmv_read_csr3(str(path).encode(), dtype_code(dtype), C.byref(buf),

@@ -377,6 +377,12 @@ int hspmv_read_csr(const char *path, int dtype, hspmv_csr_buf *out);
 /* Text .csr3 reader (reformat-csr-to-csr3/stats.c:10-79 layout). */
 int hspmv_read_csr3(const char *path, int dtype, hspmv_csr_buf *A,
                     hspmv_csr3_buf *maps);
+/* Matrix Market coordinate reader (the input of the reference's converter,
+ * helpers/converter.m:1-50 with helpers/mmread.m): field real | integer |
+ * pattern, symmetry general | symmetric | skew-symmetric (symmetric files
+ * expanded as A + A.' - diag(diag(A)), mmread.m:207-209); duplicates summed,
+ * exact zeros dropped, columns sorted per row (helpers/sparse2csr.m). */
+int hspmv_read_mtx(const char *path, int dtype, hspmv_csr_buf *out);
 /* Writers (reference text layouts: helpers/sparse2csr.m:1-7 for .csr,
  * reformat-csr-to-csr3/spmv-auto.cpp:30-65 for .csr3; values "%.6f"). */
 int hspmv_write_csr(const char *path, const hspmv_csr *A);
@@ -418,6 +424,12 @@ int hspmv_build_csr3_bandk(const hspmv_csr *A, int ssrs, int srs, hspmv_csr_buf 
 int hspmv_build_csr2_maps(const hspmv_csr *A, int super_row_size, hspmv_csr3_buf *out);
 int hspmv_build_csr2_bandk(const hspmv_csr *A, int super_row_size, hspmv_csr_buf *A_out,
                            hspmv_csr3_buf *maps_out, int32_t *perm);
+/* Reverse Cuthill-McKee of A's symmetrised pattern: the ordering the
+ * reference's converter applies before writing X.mtx.rcm.csr
+ * (helpers/converter.m:14-15, Octave symrcm; tie-breaking not pinned).
+ * Outputs P A P^T (columns sorted; free with hspmv_free_csr) and, if
+ * perm != NULL, perm[m]: new row i is row perm[i] of A.  A must be square. */
+int hspmv_rcm_reorder(const hspmv_csr *A, hspmv_csr_buf *A_out, int32_t *perm);
 /* Auto parameters.  flavour 0: the .csr3 writer / Volta formula
  * (reformat-csr-to-csr3/spmv-auto.cpp:154-173); 1: the MI100 driver formula
  * (hip/spmv-auto-mi100.cu:130-158); 2: this library's MI355X choice. */
