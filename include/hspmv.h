@@ -38,7 +38,8 @@ extern "C" {
 #define HSPMV_VERSION_MINOR 3  /* 0.2: hspmv_options, info.deterministic;
                                   0.3: info.rccl_version / csort chunks,
                                   hspmv_get_info fills the 0.1 layout only,
-                                  hspmv_xdict_plan_ex, hspmv_rccl_version */
+                                  hspmv_xdict_plan_ex, hspmv_rccl_version,
+                                  hspmv_read_mtx, hspmv_rcm_reorder */
 
 /* ---------------------------------------------------------------- status */
 #define HSPMV_OK 0
