@@ -172,3 +172,25 @@ def test_cli_gflops_printed_from_timemin():
     kg = harness_value(p.stdout, "KernelGFLOPs:")
     assert abs(kg - 2.0 * A.nnz / kmin * 1e-9) <= 1e-5 * kg
     assert "KernelGBps:" in p.stdout and "GBps:" in p.stdout
+
+
+@pytest.mark.gpu
+def test_reference_pipeline_mtx_to_spmv(tmp_path):
+    """The reference's whole input pipeline with this framework's tools:
+    .mtx -> (mtx2csr, converter.m's role) .csr + .rcm.csr -> (reformat-auto)
+    .csr3 -> spmv-csr / spmv-csrk, each run's y checked by the driver."""
+    import scipy.io
+    import scipy.sparse as sp
+    import hspmv
+    A = gen.stencil27(20, rcm=False)
+    S = sp.csr_matrix((A.val, A.col_idx, A.row_ptr), shape=(A.m, A.n))
+    mtx = tmp_path / "s27.mtx"
+    scipy.io.mmwrite(str(mtx), sp.tril(S), symmetry="symmetric")
+    csr, rcm, csr3 = tmp_path / "s27.mtx.csr", tmp_path / "s27.mtx.rcm.csr", tmp_path / "s27.mtx.rcm.csr3"
+    run(BUILD / "mtx2csr", mtx, csr, rcm)
+    run(BUILD / "reformat-auto", rcm, csr3)
+    for tool, f in (("spmv-csr", csr), ("spmv-csr", rcm), ("spmv-csrk", rcm), ("spmv-csrk", csr3)):
+        p = run(BUILD / tool, f, 5, "--x", "rand:4")
+        assert "Number Wrong: 0" in p.stdout and "Check: PASS" in p.stdout, (tool, f, p.stdout)
+        harness_parse(p.stdout)
+    assert hspmv.read_csr(rcm).nnz == A.nnz
