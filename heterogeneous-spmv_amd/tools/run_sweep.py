@@ -22,6 +22,12 @@ manual sizes, as run_tuning.py:126 does.
         [--schedules auto,stream,csr3,vector] [--gpus 1] [--num-runs 20]
         [--sizes 20x10,7x8] [--out DIR] [--record sweep.csv] [--timeout 600]
     python .../run_sweep.py --synthetic c2,c3 ...   # writes the configs as .csr first
+    python .../run_sweep.py --mtx DIR [--csr3] ...   # SuiteSparse .mtx files first
+
+--mtx runs the reference's conversion steps on every DIR/*.mtx before the
+sweep, with this build's tools: mtx2csr (helpers/converter.m: X.mtx.csr and
+the RCM-ordered X.mtx.rcm.csr) and, with --csr3, reformat-auto
+(reformat-csr-to-csr3/convert-all.sh: X.mtx.rcm.csr3).
 
 Matrices: every *.csr / *.csr3 / *.bin file in DIR (".csr3" carry their own
 maps).  A run that times out is reported and skipped, like run_norm.py:86-89.
@@ -77,10 +83,24 @@ def synthetic(configs, where: Path):
             hspmv.write_csr(where / f"{cfg}.csr", A)
 
 
+def convert_mtx(src: Path, where: Path, build: Path, csr3: bool, timeout: float) -> None:
+    """converter.m + convert-all.sh for every src/*.mtx, into `where`."""
+    where.mkdir(parents=True, exist_ok=True)
+    for f in sorted(src.glob("*.mtx")):
+        norm, rcm = where / f"{f.name}.csr", where / f"{f.name}.rcm.csr"
+        subprocess.run([str(build / "mtx2csr"), str(f), str(norm), str(rcm)], check=True,
+                       timeout=timeout)
+        if csr3:
+            subprocess.run([str(build / "reformat-auto"), str(rcm), str(where / f"{f.name}.rcm.csr3")],
+                           check=True, capture_output=True, timeout=timeout)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--matrices", default="")
     ap.add_argument("--synthetic", default="", help="configs to generate (tools/sweep.py names)")
+    ap.add_argument("--mtx", default="", help="directory of .mtx files to convert first")
+    ap.add_argument("--csr3", action="store_true", help="with --mtx: also reformat-auto to .csr3")
     ap.add_argument("--drivers", default="spmv-csr,spmv-csrk")
     ap.add_argument("--schedules", default="auto")
     ap.add_argument("--gpus", default="1")
@@ -97,6 +117,8 @@ def main(argv=None):
     mdir = Path(a.matrices) if a.matrices else out / "matrices"
     if a.synthetic:
         synthetic(a.synthetic.split(","), mdir)
+    if a.mtx:
+        convert_mtx(Path(a.mtx), mdir, Path(a.build), a.csr3, a.timeout)
     mats = sorted(p for p in mdir.iterdir() if p.suffix in (".csr", ".csr3", ".bin"))
     record = out / a.record
     sizes = [tuple(s.split("x")) for s in a.sizes.split(",")] if a.sizes else [None]

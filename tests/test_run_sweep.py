@@ -96,3 +96,25 @@ def test_sweep_on_golden_matrices(tmp_path):
         t = [float(v) for v in (r[5:8] if r[0] == "spmv-csrk" else r[4:7])]
         assert 0 < t[0] <= t[2] <= t[1]
         assert r[-2] == "PASS"
+
+
+def test_mtx_inputs_are_converted_first(tmp_path):
+    """--mtx: the reference's conversion steps (converter.m, convert-all.sh)
+    with the real host-only converters, then the (stand-in) drivers."""
+    import scipy.io
+    import scipy.sparse as sp
+    src = tmp_path / "mm"
+    src.mkdir()
+    S = sp.random(300, 300, density=0.02, random_state=1, format="csr") + sp.eye(300)
+    scipy.io.mmwrite(str(src / "r300.mtx"), S)
+    b = fake_build(tmp_path)
+    for tool in ("mtx2csr", "reformat-auto"):
+        (b / tool).symlink_to(REPO / "heterogeneous-spmv_amd" / "build" / tool)
+    out = tmp_path / "out"
+    rc = run_sweep.main(["--mtx", str(src), "--csr3", "--build", str(b), "--out", str(out),
+                         "--drivers", "spmv-csr", "--num-runs", "3"])
+    assert rc == 0
+    names = sorted(p.name for p in (out / "matrices").iterdir())
+    assert names == ["r300.mtx.csr", "r300.mtx.rcm.csr", "r300.mtx.rcm.csr3"]
+    rows = (out / "sweep.csv").read_text().splitlines()
+    assert [r.split(", ")[1] for r in rows] == names
