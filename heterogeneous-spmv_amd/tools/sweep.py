@@ -110,6 +110,9 @@ def build(cfg):
         A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32, rcm=cfg == "c5r")
         maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
         return A, maps, "C5 power-law 2e6 rows CSR-3 fp32" + (" RCM-permuted" if cfg == "c5r" else "")
+    import auto_regret  # the planner-regret zoo's shapes (urand8, diag, tall, ...)
+    if cfg in auto_regret.EXTRA:
+        return auto_regret.build(cfg)
     raise ValueError(cfg)
 
 
@@ -198,6 +201,19 @@ def group_variants(A):
     return v
 
 
+def short_row_variants(A):
+    """STREAM launch shapes for short rows: groups per wave x chunk size x
+    waves per workgroup (hspmv_options.stream_waves)."""
+    v = [("stream-auto", dict(kernel="stream"), None)]
+    for w in (1, 2, 4):
+        for g in (1, 2, 4):
+            for u in (0, 2, 4):
+                name = f"stream-w{w}-g{g}" + (f"-u{u}" if u else "")
+                v.append((name, dict(kernel="stream", groups_per_wave=g, chunk_u=u,
+                                     options={"stream_waves": w}), None))
+    return v
+
+
 def c16_variants(A, maps):
     """16-bit column offsets (default) vs 32-bit columns, over chunk sizes."""
     d = A.nnz / A.m
@@ -220,7 +236,7 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--out", default="")
     ap.add_argument("--quick", action="store_true", help="only stream u4/u6 + csr3 auto")
-    ap.add_argument("--grid", default="main", choices=["main", "xcd", "groups", "c16"],
+    ap.add_argument("--grid", default="main", choices=["main", "xcd", "groups", "c16", "short"],
                     help="xcd: the XCD chunk grid (blocks per XCD turn) at the auto chunk size")
     a = ap.parse_args()
     import oracle
@@ -236,7 +252,7 @@ def main():
         ops = []
         vs = {"main": lambda: variants(cfg, A, maps), "xcd": lambda: xcd_variants(A, maps),
               "groups": lambda: group_variants(A),
-              "c16": lambda: c16_variants(A, maps)}[a.grid]()
+              "c16": lambda: c16_variants(A, maps), "short": lambda: short_row_variants(A)}[a.grid]()
         if a.quick:
             vs = [v for v in vs if v[0] in ("stream-u4", "stream-u6", "stream-u8", "stream-auto",
                                           "stream-auto-noxcd", "csr3-auto", "csr3-mi355x-auto")]
