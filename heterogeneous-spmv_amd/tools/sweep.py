@@ -73,6 +73,10 @@ def build(cfg):
     if cfg == "c4":
         sh = hdist.build_shard("c4", 0, 8)
         return sh.A, None, "C4 banded 2e7 rows, rank-0 shard of 8 (2.5M rows) fp64"
+    if cfg.startswith("c4p"):  # C4's rank-0 shard at P ranks (c4p2 / c4p4), or the whole (c4p1)
+        P = int(cfg[3:])
+        sh = hdist.build_shard("c4", 0, P)
+        return sh.A, None, f"C4 banded 2e7 rows, rank-0 shard of {P} fp64"
     if cfg == "b27":  # diagnostic: C3's row length with a C4-like (local) gather
         A = gen.banded(1_953_125, per_row=27, half=32, seed=5)
         return A, None, "diag: banded 1.95M rows, 27 nnz/row within +-32, fp64"
@@ -214,6 +218,14 @@ def short_row_variants(A):
     return v
 
 
+def waves_variants(A):
+    """STREAM waves per workgroup at the planner's other choices."""
+    v = [("stream-auto", dict(kernel="stream"), None)]
+    for w in (1, 2, 4):
+        v.append((f"stream-w{w}", dict(kernel="stream", options={"stream_waves": w}), None))
+    return v
+
+
 def c16_variants(A, maps):
     """16-bit column offsets (default) vs 32-bit columns, over chunk sizes."""
     d = A.nnz / A.m
@@ -236,7 +248,7 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--out", default="")
     ap.add_argument("--quick", action="store_true", help="only stream u4/u6 + csr3 auto")
-    ap.add_argument("--grid", default="main", choices=["main", "xcd", "groups", "c16", "short"],
+    ap.add_argument("--grid", default="main", choices=["main", "xcd", "groups", "c16", "short", "waves"],
                     help="xcd: the XCD chunk grid (blocks per XCD turn) at the auto chunk size")
     a = ap.parse_args()
     import oracle
@@ -252,7 +264,8 @@ def main():
         ops = []
         vs = {"main": lambda: variants(cfg, A, maps), "xcd": lambda: xcd_variants(A, maps),
               "groups": lambda: group_variants(A),
-              "c16": lambda: c16_variants(A, maps), "short": lambda: short_row_variants(A)}[a.grid]()
+              "c16": lambda: c16_variants(A, maps), "short": lambda: short_row_variants(A),
+              "waves": lambda: waves_variants(A)}[a.grid]()
         if a.quick:
             vs = [v for v in vs if v[0] in ("stream-u4", "stream-u6", "stream-u8", "stream-auto",
                                           "stream-auto-noxcd", "csr3-auto", "csr3-mi355x-auto")]
