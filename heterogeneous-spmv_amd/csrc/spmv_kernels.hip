@@ -303,13 +303,16 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
       const int64_t waves = (tasks + p.groups - 1) / p.groups;
       // waves per workgroup.  The STREAM waves never meet at a barrier, so
       // small workgroups free their CU slots wave by wave: one wave per
-      // workgroup for Infinity-Cache-resident matrices and LDS-windowed
-      // gathers (C2 bench 737 -> 760 GFLOP/s, C4 53.2 -> 50.4 us), two for
-      // HBM gathers, where one-wave workgroups run into the per-CU workgroup
-      // limit (honeycomb 166.0 -> 161.8 us with two, flat with one; l4k
-      // 211.2 -> 207.5).  Four (the dictionaries' 256-row blocks) with x
-      // dictionaries; profiles/r01_ab_stream_w.jsonl.
-      p.waves_per_block = A.has_xdict ? 4 : ((footprint <= 192.0 * 1024 * 1024 || A.has_xwin) ? 1 : 2);
+      // workgroup for Infinity-Cache-resident matrices (C2 bench 737 -> 760
+      // GFLOP/s), two for HBM-resident ones, where one-wave workgroups run
+      // into the per-CU workgroup limit (honeycomb 166.0 -> 161.8 us with
+      // two, flat with one; l4k 211.2 -> 207.5; profiles/r01_ab_stream_w.jsonl).
+      // LDS-windowed HBM matrices took one wave until r04 (C4 53.2 -> 50.4
+      // us in r01); on today's kernel two measure 47.1 vs 47.7-48.0 on C4's
+      // 8-rank shard and tie at 4 / 2 / 1 ranks (profiles/r04/
+      // sweep_stream_waves.jsonl, 7 rounds, one process).  Four (the
+      // dictionaries' 256-row blocks) with x dictionaries.
+      p.waves_per_block = A.has_xdict ? 4 : (footprint <= 192.0 * 1024 * 1024 ? 1 : 2);
       if ((t.stream_waves == 1 || t.stream_waves == 2 || t.stream_waves == 4) && !A.has_xdict)
         p.waves_per_block = t.stream_waves;
       p.blocks = (waves + p.waves_per_block - 1) / p.waves_per_block;

@@ -699,7 +699,7 @@ def test_full_size_fp32_bitwise_vs_reference_omp_spmv(cfg):
 
 def test_stream_workgroup_sizes_identical():
     """STREAM with 1, 2 and 4 waves per workgroup (options stream_waves; the
-    planner picks 1 for cache-resident / x-windowed matrices, 2 otherwise,
+    planner picks 1 for cache-resident matrices, 2 for HBM-resident ones,
     4 with x dictionaries): bit-identical y, including x windows, several
     groups per wave, split rows and a row count that is not a multiple of
     64."""
