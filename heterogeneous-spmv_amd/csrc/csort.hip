@@ -23,7 +23,7 @@
 // run to run except where an fp64 sum sits within an fp64 rounding of an
 // fp32 tie), fp64 results agree with it to the fp64 rounding of the sum.
 //
-// Layout (built on the host, hspmv_api.cpp build_csort): entries padded to
+// Layout (built on the host, hspmv_csort_build.cpp build_csort): entries padded to
 // whole chunks of 64*U; per chunk a base column (cbase); per entry idx =
 // slot << 16 | (col - base) (a chunk never spans more than 65535 columns)
 // and the value: fp32 as one 8-byte {idx, val} record (one load per

@@ -1,4 +1,5 @@
-// Host-side helpers shared by hspmv_api.cpp and hspmv_io.cpp.
+// Host-side helpers shared by the host runtime units (hspmv_runtime.h) and
+// the I/O units (hspmv_io.cpp, hspmv_mtx.cpp, hspmv_bandk.cpp).
 #pragma once
 #include <stdarg.h>
 #include <stdint.h>

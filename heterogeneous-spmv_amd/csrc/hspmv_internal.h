@@ -1,4 +1,4 @@
-// Internal interfaces shared by the host runtime (hspmv_api.cpp) and the
+// Internal interfaces shared by the host runtime (hspmv_runtime.h units) and the
 // HIP kernels (spmv_kernels.hip).  Not part of the C ABI.
 #pragma once
 #include <hip/hip_runtime_api.h>
@@ -41,7 +41,7 @@ struct DevCSR {
 // (include/hspmv.h; 0 = the library's choice); the second holds A/B-only
 // knobs that product builds never change: only a diagnostic build
 // (make diag-env: -DHSPMV_ENV_KNOBS) reads them, and the public fields, from
-// HSPMV_* environment variables (tuning_from_env, hspmv_api.cpp), so a
+// HSPMV_* environment variables (tuning_from_env, hspmv_options.cpp), so a
 // production handle's kernel choice cannot move with the environment.
 struct Tuning {
   int csr3_plan = 0;        // 0/1 aligned 64-row tasks, 2 packed super-rows, 3 workgroup per SSR
@@ -92,7 +92,7 @@ constexpr int32_t kLongChunk = 4096;
 // b % H (a fixed slice of x) and walks chunks [blk_c[b], blk_c[b+1]) of 64*u
 // entries in column order; its rows are [blk_r[2b], blk_r[2b+1]) (each part
 // has its own row partition) and its long-row slices vslice[blk_v[b] ..
-// blk_v[b+1]).  Built by build_csort (hspmv_api.cpp).
+// blk_v[b+1]).  Built by build_csort (hspmv_csort_build.cpp).
 constexpr int kCsortThreads = 1024;
 constexpr int kCsortMaxLds = 160 * 1024;
 struct DevCsort {

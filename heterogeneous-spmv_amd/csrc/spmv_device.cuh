@@ -394,7 +394,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         unsigned long long cm = coop ? coop & __ballot(end > c && beg <= c + last) : 0ull;
         // three or more pieces (rows of 33..~100 nonzeros): four at a time,
         // one 16-lane DPP row each.  CSR3 kernel only -- the tasks that
-        // mid-density CSR matrices run as (hspmv_api.cpp build_tasks): in
+        // mid-density CSR matrices run as (hspmv_tables.cpp build_tasks): in
         // the STREAM kernel the extra code cost the honeycomb matrix 4 %
         // (161 -> 168 us) with no such rows at all (r02z9).  d33 173 ->
         // 137 us, d48 132 -> 109, d64 103 -> 95 (profiles/r02z8).
@@ -484,7 +484,7 @@ __device__ __forceinline__ void stage_xwin(T *xs, const T *__restrict__ x, int32
 // in runs: {x_start, lds_off} per run, then a sentinel {0, total}; run i
 // stages x[x_start, x_start + len) at xs[lds_off ...], len = the next
 // record's lds_off - lds_off.  The col stream then holds each nonzero's
-// 16-bit position in xs (the host builds both, hspmv_api.cpp build_xdict).
+// 16-bit position in xs (the host builds both, hspmv_xdict.cpp build_xdict).
 struct XDict {
   const int32_t *blk;
   const int2 *runs;

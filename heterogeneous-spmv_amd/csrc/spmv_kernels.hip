@@ -30,7 +30,7 @@
 //      packed into <= 64-row tasks (HSPMV_TASK_FILL=0), or one workgroup of
 //      W waves per super-super-row whose super-rows are split W ways by
 //      nonzeros (HSPMV_CSR3_PLAN=ssr); each wave runs the stream routine
-//      over its task (hspmv_api.cpp build_tasks).  Replaces cuSpMV_3 / cuSpMV_3_vec (thread or
+//      over its task (hspmv_tables.cpp build_tasks).  Replaces cuSpMV_3 / cuSpMV_3_vec (thread or
 //      sub-warp per row inside (8,12)-thread blocks, csrk.cu:185-319) and
 //      cuSpMV_2 (degenerate outer level).
 //
@@ -268,7 +268,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
     // blocks: 112.3 / 105.8 / 109.4 / 109.6; profiles/r02k_ab_xcd.jsonl)
     chunk = 4;
   // (packed tasks without super-super-rows: a CSR matrix whose 64-row
-  // groups exceed the task budget, hspmv_api.cpp build_tasks)
+  // groups exceed the task budget, hspmv_tables.cpp build_tasks)
   const bool tasks = A.n_ssr > 0 || packed_tasks > 0;
   if (k == kAuto)
     p.kernel = A.has_csort ? kCsort : (tasks ? kCsr3 : kStream);
