@@ -172,3 +172,33 @@ def test_csr2_maps_are_the_first_level_of_the_csr3_grouping():
         assert np.array_equal(maps.outer, np.arange(maps.n_sr + 1))
     with pytest.raises(hspmv.HspmvError):
         hspmv.build_csr2_maps(gen.laplace2d(4, 4), 0)
+
+
+def test_writers_match_printf_formatting(tmp_path):
+    """The parallel writers print what the reference's fprintf calls print:
+    "%d " indices and "%f " (.csr) / "%.6f " (.csr3) values -- checked
+    against Python's %-formatting (correctly rounded, as glibc's printf) on
+    values that stress the rounding: tiny, huge, negative zero, halfway
+    cases."""
+    rng = np.random.default_rng(11)
+    m = 2000
+    lens = rng.integers(0, 9, m)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ci = rng.integers(0, m, rp[-1]).astype(np.int32)
+    v = rng.uniform(-1, 1, rp[-1]) * 10.0 ** rng.integers(-9, 12, rp[-1])
+    v[:8] = [-0.0, 0.0, 1e20, -1e-7, 5e-7, 0.0000025, 123456.0000005, -2.5e-6]
+    A = hspmv.CsrMatrix(m, m, rp, ci, v)
+    maps = hspmv.build_csr3_maps(A, 7, 8)
+    hspmv.write_csr(tmp_path / "a.csr", A)
+    hspmv.write_csr3(tmp_path / "a.csr3", A, maps)
+    ints = lambda a: "".join(f"{int(t)} " for t in a)  # noqa: E731
+    want = (f"{m} {m} {A.nnz}\n" + ints(rp) + "\n" + ints(ci) + "\n"
+            + "".join("%f " % t for t in v) + "\n")
+    assert (tmp_path / "a.csr").read_text() == want
+    want3 = (f"{maps.n_ssr} {maps.n_sr} {m} {m} {A.nnz} \n" + ints(maps.outer) + ints(maps.inner)
+             + ints(rp) + ints(ci) + "".join("%.6f " % t for t in v))
+    assert (tmp_path / "a.csr3").read_text() == want3
+    # fp32 values print their float's exact decimal
+    hspmv.write_csr(tmp_path / "b.csr", A.astype(np.float32))
+    vals = (tmp_path / "b.csr").read_text().split("\n")[3].split()
+    assert vals == ["%f" % t for t in v.astype(np.float32).astype(np.float64)]
