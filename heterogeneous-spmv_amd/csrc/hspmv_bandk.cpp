@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #include "hspmv_common.h"
@@ -280,6 +281,17 @@ void uncoarsen(std::vector<int32_t> &map, const std::vector<int32_t> &perm_coars
   for (size_t i = 0; i < perm_finer.size(); ++i) perm_finer[i] = old_perm[(size_t)np[i]];
 }
 
+// body(r0, r1) over [0, n) split into contiguous ranges, one thread each.
+template <typename F>
+void par_ranges(int64_t n, F body) {
+  const unsigned hc = std::thread::hardware_concurrency();
+  const int64_t T = std::max<int64_t>(1, std::min<int64_t>({16, hc ? (int64_t)hc : 4, n / 65536 + 1}));
+  std::vector<std::thread> th;
+  for (int64_t t = 1; t < T; ++t) th.emplace_back([&, t]() { body(n * t / T, n * (t + 1) / T); });
+  body(0, n / T);
+  for (auto &x : th) x.join();
+}
+
 // reorderA (csrk.cu:722-870): new row i = row perm0[i] of A, columns
 // renumbered by the inverse permutation and sorted per row, values moved.
 int permute_symmetric(const hspmv_csr *A, const std::vector<int32_t> &perm0, hspmv_csr_buf *A_out) {
@@ -303,19 +315,23 @@ int permute_symmetric(const hspmv_csr *A, const std::vector<int32_t> &perm0, hsp
     const int32_t o = perm0[(size_t)i];
     A_out->row_ptr[i + 1] = A_out->row_ptr[i] + (A->row_ptr[o + 1] - A->row_ptr[o]);
   }
-  std::vector<std::pair<int32_t, int32_t>> row;
-  for (int64_t i = 0; i < m; ++i) {
-    const int32_t o = perm0[(size_t)i];
-    row.clear();
-    for (int32_t k = A->row_ptr[o]; k < A->row_ptr[o + 1]; ++k) row.push_back({fwd[(size_t)A->col_idx[k]], k});
-    std::sort(row.begin(), row.end());
-    int32_t at = A_out->row_ptr[i];
-    for (const auto &e : row) {
-      A_out->col_idx[at] = e.first;
-      memcpy((char *)A_out->val + sv * (size_t)at, (const char *)A->val + sv * (size_t)e.second, sv);
-      ++at;
+  // rows are independent: row ranges in parallel (the .csr3 builds of the
+  // 50-200 M-nonzero configurations spend most of their time here)
+  par_ranges(m, [&](int64_t r0, int64_t r1) {
+    std::vector<std::pair<int32_t, int32_t>> row;
+    for (int64_t i = r0; i < r1; ++i) {
+      const int32_t o = perm0[(size_t)i];
+      row.clear();
+      for (int32_t k = A->row_ptr[o]; k < A->row_ptr[o + 1]; ++k) row.push_back({fwd[(size_t)A->col_idx[k]], k});
+      std::sort(row.begin(), row.end());
+      int32_t at = A_out->row_ptr[i];
+      for (const auto &e : row) {
+        A_out->col_idx[at] = e.first;
+        memcpy((char *)A_out->val + sv * (size_t)at, (const char *)A->val + sv * (size_t)e.second, sv);
+        ++at;
+      }
     }
-  }
+  });
   return HSPMV_OK;
 }
 
@@ -439,13 +455,23 @@ extern "C" int hspmv_rcm_reorder(const hspmv_csr *A, hspmv_csr_buf *A_out, int32
             adj[(size_t)fill[(size_t)A->col_idx[k]]++] = (int32_t)r;
           }
     }
+    // per-vertex sort + de-duplication in parallel, then compaction
+    std::vector<int64_t> ulen((size_t)m, 0);
+    par_ranges(m, [&](int64_t r0, int64_t r1) {
+      for (int64_t r = r0; r < r1; ++r) {
+        auto b = adj.begin() + cnt[(size_t)r], e = adj.begin() + cnt[(size_t)r + 1];
+        std::sort(b, e);
+        ulen[(size_t)r] = std::unique(b, e) - b;
+      }
+    });
     g.r.assign((size_t)m + 1, 0);
-    for (int64_t r = 0; r < m; ++r) {
-      auto b = adj.begin() + cnt[(size_t)r], e = adj.begin() + cnt[(size_t)r + 1];
-      std::sort(b, e);
-      g.c.insert(g.c.end(), b, std::unique(b, e));
-      g.r[(size_t)r + 1] = (int64_t)g.c.size();
-    }
+    for (int64_t r = 0; r < m; ++r) g.r[(size_t)r + 1] = g.r[(size_t)r] + ulen[(size_t)r];
+    g.c.resize((size_t)g.r[(size_t)m]);
+    par_ranges(m, [&](int64_t r0, int64_t r1) {
+      for (int64_t r = r0; r < r1; ++r)
+        std::copy(adj.begin() + cnt[(size_t)r], adj.begin() + cnt[(size_t)r] + ulen[(size_t)r],
+                  g.c.begin() + g.r[(size_t)r]);
+    });
     std::vector<int32_t>().swap(adj);
     g.deg.assign(g.c.size(), 1);
     std::vector<int32_t> order;
