@@ -226,6 +226,19 @@ def waves_variants(A):
     return v
 
 
+def det_variants(A, maps):
+    """Deterministic handles (options deterministic=1: no csort) against AUTO:
+    the row kernels with and without the CSR-3 maps, x slabs on / off."""
+    v = [("auto", dict(kernel="auto"), maps)]
+    for tag, mp in (("maps", maps), ("nomaps", None)):
+        if tag == "maps" and maps is None:
+            continue
+        v.append((f"det-{tag}", dict(kernel="auto", options={"deterministic": 1}), mp))
+        v.append((f"det-{tag}-noslabs", dict(kernel="auto", options={"deterministic": 1, "x_slabs": -1}), mp))
+    v.append(("det-stream", dict(kernel="stream", options={"deterministic": 1}), None))
+    return v
+
+
 def c16_variants(A, maps):
     """16-bit column offsets (default) vs 32-bit columns, over chunk sizes."""
     d = A.nnz / A.m
@@ -248,7 +261,7 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--out", default="")
     ap.add_argument("--quick", action="store_true", help="only stream u4/u6 + csr3 auto")
-    ap.add_argument("--grid", default="main", choices=["main", "xcd", "groups", "c16", "short", "waves"],
+    ap.add_argument("--grid", default="main", choices=["main", "xcd", "groups", "c16", "short", "waves", "det"],
                     help="xcd: the XCD chunk grid (blocks per XCD turn) at the auto chunk size")
     a = ap.parse_args()
     import oracle
@@ -265,7 +278,7 @@ def main():
         vs = {"main": lambda: variants(cfg, A, maps), "xcd": lambda: xcd_variants(A, maps),
               "groups": lambda: group_variants(A),
               "c16": lambda: c16_variants(A, maps), "short": lambda: short_row_variants(A),
-              "waves": lambda: waves_variants(A)}[a.grid]()
+              "waves": lambda: waves_variants(A), "det": lambda: det_variants(A, maps)}[a.grid]()
         if a.quick:
             vs = [v for v in vs if v[0] in ("stream-u4", "stream-u6", "stream-u8", "stream-auto",
                                           "stream-auto-noxcd", "csr3-auto", "csr3-mi355x-auto")]
@@ -302,6 +315,7 @@ def main():
                    "chunk_u": op.info["chunk_u"], "waves_per_block": op.info["waves_per_block"],
                    "n_split_rows": op.info["n_split_rows"], "xcd_chunk": op.info["xcd_remap"],
                    "groups": op.info["groups_per_wave"], "col16": op.info["col16"],
+                   "x_slabs": op.info["x_slabs"], "x_dict": op.info["x_dict"],
                    "format_gbps_min": round(op.info["format_bytes"] / tmin * 1e-9, 1),
                    "desc": desc}
             lines.append(rec)
