@@ -436,6 +436,27 @@ bool irregular_gathers(const int32_t *rp, const int32_t *col, int64_t m, double 
   return lines >= 32 * sampled;
 }
 
+// Median over (up to 16 K sampled) 64-row groups of the columns a group
+// spans (max - min + 1; empty groups skipped).
+double median_group_span(const int32_t *rp, const int32_t *col, int64_t m) {
+  const int64_t groups = (m + 63) / 64;
+  const int64_t step = std::max<int64_t>(1, groups / 16384);
+  std::vector<int64_t> spans;
+  for (int64_t g = 0; g < groups; g += step) {
+    const int64_t r0 = g * 64, r1 = std::min(m, r0 + 64);
+    int32_t lo = INT32_MAX, hi = -1;
+    for (int64_t r = r0; r < r1; ++r)
+      for (int32_t k = rp[r]; k < rp[r + 1]; ++k) {
+        lo = std::min(lo, col[k]);
+        hi = std::max(hi, col[k]);
+      }
+    if (hi >= lo) spans.push_back((int64_t)hi - lo + 1);
+  }
+  if (spans.empty()) return 0.0;
+  std::nth_element(spans.begin(), spans.begin() + (ptrdiff_t)(spans.size() / 2), spans.end());
+  return (double)spans[spans.size() / 2];
+}
+
 constexpr double kSlabBytes = 2.0 * 1024 * 1024;
 constexpr int kMaxSlabs = 32;
 
@@ -467,6 +488,13 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
     const double extra = (double)(B - 1) * (4.0 * (double)(m + 1) + 2.0 * sv * (double)m);
     if (extra > 0.25 * (double)nnz * (sv + 4.0) || (double)nnz / B < 2.0e6) return HSPMV_OK;
     if (!irregular_gathers(rp, col, m, sv)) return HSPMV_OK;
+    // ... and only when the x a row group gathers from is wider than an
+    // XCD's L2 (median 64-row group column span > 4 MiB of x): scattered but
+    // local gathers (a +-4000 band of random columns, `mix`) stay L2 hits
+    // without slabs, and the extra passes only cost (deterministic handles
+    // on mix: 284 us with four slabs vs 209 without; profiles/r04/
+    // sweep_deterministic.jsonl)
+    if (median_group_span(rp, col, m) * sv <= 4.0 * 1024 * 1024) return HSPMV_OK;
   }
   // per (slab, row) segment lengths; rows must be slab-monotone
   std::vector<int32_t> srp((size_t)B * (size_t)(m + 1), 0);
