@@ -23,8 +23,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cctype>
 #include <charconv>
 #include <cstdlib>
+#include <string>
 #include <thread>
 #include <vector>
 
