@@ -185,7 +185,8 @@ extern "C" int hspmv_read_mtx(const char *path, int dtype, hspmv_csr_buf *out) {
     std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
     for (const auto &v : part)
       for (const Entry &en : v) {
-        rowbuf[(size_t)fill[(size_t)en.r]++] = {en.c, en.v};
+        // skew-symmetric: a stored diagonal entry cancels in A - A.' (0 is dropped)
+        rowbuf[(size_t)fill[(size_t)en.r]++] = {en.c, sym < 0 && en.r == en.c ? 0.0 : en.v};
         if (sym != 0 && en.r != en.c) rowbuf[(size_t)fill[(size_t)en.c]++] = {en.r, sym > 0 ? en.v : -en.v};
       }
   }

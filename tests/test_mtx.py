@@ -31,6 +31,10 @@ def run(*args, check=True):
 
 def expected(path):
     S = sp.csr_matrix(scipy.io.mmread(str(path)))
+    if "skew-symmetric" in open(path).readline().lower():
+        # mmread.m forms A - A.' (helpers/mmread.m:214-216): a stored diagonal
+        # entry cancels; scipy keeps it
+        S = S - sp.diags(S.diagonal())
     S.sum_duplicates()
     S.eliminate_zeros()
     S.sort_indices()
@@ -74,9 +78,10 @@ MTX = {
 5 3
 """,
     "skew_integer": """%%MatrixMarket matrix coordinate integer skew-symmetric
-3 3 2
+3 3 3
 2 1 3
 3 1 -4
+2 2 5
 """,
 }
 
