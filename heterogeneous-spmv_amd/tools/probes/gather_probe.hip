@@ -10,7 +10,7 @@
 // Every wave issues the same number of gather instructions (8 in flight per
 // batch, like csort's U); instruction i of a wave starts at a base that
 // advances by the pattern's span, so each instruction touches lines the CU
-// has not read yet (L2 hits, "sweep"), or stays inside a 16 KiB window that
+// has not read yet (L2 hits, "sweep", within 2 MiB), or stays inside a 16 KiB window that
 // the L1 keeps ("hot").  Lane l of an instruction reads, relative to base:
 //   line2   : l                         64 floats: 8 sectors, 2 lines (coalesced)
 //   one     : 0                         1 sector
@@ -84,9 +84,11 @@ __global__ __launch_bounds__(kThreads) void probe(const float *__restrict__ x, f
     for (int u = 0; u < kBatch; ++u) {
       const long i = i0 + u;
       long base = ((i * kWaves + wid) * S);
-      // (window / limit are kernel arguments: a compile-time modulus lets the
-      // compiler see repeated addresses and merge the loads)
-      base = HOT ? base % window : base % limit;
+      // (window / limit are power-of-two masks passed as kernel arguments: a
+      // compile-time modulus lets the compiler merge repeated loads, a
+      // runtime 64-bit modulus costs more VALU than the cheap patterns'
+      // gathers themselves)
+      base = HOT ? (base & window) : (base & limit);
       v[u] = xh[base + off];
     }
 #pragma unroll
@@ -103,8 +105,8 @@ float run(const float *x, float *out, hipStream_t st) {
   float best = 1e30f;
   for (int it = 0; it < 12; ++it) {
     (void)hipEventRecord(a, st);
-    hipLaunchKernelGGL((probe<MODE, HOT>), dim3(kBlocks), dim3(kThreads), 0, st, x, out, (long)kHotWindow,
-                       kHalf - 4096);
+    hipLaunchKernelGGL((probe<MODE, HOT>), dim3(kBlocks), dim3(kThreads), 0, st, x, out,
+                       (long)kHotWindow - 1, kHalf / 2 - 1);
     (void)hipEventRecord(z, st);
     (void)hipEventSynchronize(z);
     float ms = 0;
