@@ -47,8 +47,14 @@ constexpr long kHalf = 1L << 20;        // fp32 entries per half (4 MiB)
 constexpr int kInstr = 2048;            // gather instructions per wave
 constexpr int kHotWindow = 4096;        // floats: 16 KiB
 
-enum { LINE2 = 0, ONE, QUAD1, QUAD2, SECTOR, LINE, C5, NMODES };
-const char *kNames[NMODES] = {"line2", "one", "quad1", "quad2", "sector", "line", "c5"};
+enum { LINE2 = 0, ONE, QUAD1, QUAD2, SECTOR, LINE, C5, C5R, SQR, NMODES };
+const char *kNames[NMODES] = {"line2", "one", "quad1", "quad2", "sector", "line", "c5", "c5+rec", "sq+rec"};
+// c5+rec : the c5 gather after a per-lane 8-byte record load (csort's entry
+//          stream, 64 entries per instruction; records from a separate buffer)
+// sq+rec : "sector quads": quad q of an instruction holds the entries of one
+//          32-byte sector (1-4, pattern averaging 1.9 as C5's ~1.9 entries
+//          per touched sector), the other lanes predicated off; active lanes
+//          load their 8-byte record (compact) and gather inside the quad's sector
 
 // offset of lane l (relative to the instruction base) and the span (floats)
 // the base advances by per instruction
@@ -60,17 +66,19 @@ __device__ __forceinline__ int lane_off(int l) {
   if constexpr (MODE == QUAD2) return 8 * ((l + 2) >> 2) + (l & 3);
   if constexpr (MODE == SECTOR) return 8 * l;
   if constexpr (MODE == LINE) return 32 * l;
+  if constexpr (MODE == SQR) return 16 * (l >> 2) + (l & 3);  // quad q: sector 2q (every other one touched)
   return (l * 16) / 3;  // C5: 64 sorted entries over ~340 columns
 }
 template <int MODE>
 constexpr int span() {
   return MODE == LINE2 ? 64 : MODE == ONE ? 8 : MODE == QUAD1 ? 128 : MODE == QUAD2 ? 136
-         : MODE == SECTOR ? 512 : MODE == LINE ? 2048 : 344;
+         : MODE == SECTOR ? 512 : MODE == LINE ? 2048 : MODE == SQR ? 256 : 344;
 }
 
 template <int MODE, bool HOT>
 __global__ __launch_bounds__(kThreads) void probe(const float *__restrict__ x, float *__restrict__ out,
-                                                  long window, long limit) {
+                                                  long window, long limit,
+                                                  const uint2 *__restrict__ rec, long rlimit) {
   const int b = blockIdx.x, wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const float *xh = x + (long)(b & 1) * kHalf;
   constexpr long S = span<MODE>();
@@ -89,13 +97,32 @@ __global__ __launch_bounds__(kThreads) void probe(const float *__restrict__ x, f
       // runtime 64-bit modulus costs more VALU than the cheap patterns'
       // gathers themselves)
       base = HOT ? (base & window) : (base & limit);
-      v[u] = xh[base + off];
+      if constexpr (MODE == C5R || MODE == SQR) {
+        // the record stream: 64 (c5+rec) or the active lanes' (sq+rec) 8-byte
+        // records of this instruction, contiguous
+        constexpr int kCnt[16] = {2, 1, 3, 2, 1, 2, 4, 1, 2, 2, 1, 3, 1, 2, 2, 2};  // mean 1.94
+        const int q = lane >> 2, sub = lane & 3;
+        int pre = 0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) pre += t < q ? kCnt[t] : 0;
+        const bool act = MODE == C5R || sub < kCnt[q];
+        const long per = MODE == C5R ? 64 : 31;
+        const long ridx = (((i * kWaves + wid) * per) & (rlimit)) + (MODE == C5R ? lane : pre + sub);
+        uint2 r = act ? rec[ridx] : make_uint2(0, 0);
+        const float xv = act ? xh[base + off + (r.x & 1)] : 0.f;
+        v[u] = xv * __uint_as_float(r.y | 0x3f800000u);
+      } else {
+        v[u] = xh[base + off];
+      }
     }
 #pragma unroll
     for (int u = 0; u < kBatch; ++u) acc += v[u];
   }
   if (acc == 123.456f) out[b * kThreads + threadIdx.x] = acc;  // keep it live
 }
+
+static uint2 *g_rec = nullptr;
+constexpr long kRec = 1L << 24;  // records (128 MiB): the stream comes from HBM
 
 template <int MODE, bool HOT>
 float run(const float *x, float *out, hipStream_t st) {
@@ -106,7 +133,7 @@ float run(const float *x, float *out, hipStream_t st) {
   for (int it = 0; it < 12; ++it) {
     (void)hipEventRecord(a, st);
     hipLaunchKernelGGL((probe<MODE, HOT>), dim3(kBlocks), dim3(kThreads), 0, st, x, out,
-                       (long)kHotWindow - 1, kHalf / 2 - 1);
+                       (long)kHotWindow - 1, kHalf / 2 - 1, g_rec, kRec / 2 - 1);
     (void)hipEventRecord(z, st);
     (void)hipEventSynchronize(z);
     float ms = 0;
@@ -135,6 +162,8 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&out, kBlocks * kThreads * sizeof(float)));
   std::vector<float> h(2 * kHalf, 1.0f);
   CK(hipMemcpy(x, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+  CK(hipMalloc(&g_rec, kRec * sizeof(uint2)));
+  CK(hipMemset(g_rec, 0, kRec * sizeof(uint2)));
   hipStream_t st;
   CK(hipStreamCreate(&st));
   auto want = [&](const char *n) {
@@ -150,6 +179,8 @@ int main(int argc, char **argv) {
   if (want("sector")) report<SECTOR>(x, out, st);
   if (want("line")) report<LINE>(x, out, st);
   if (want("c5")) report<C5>(x, out, st);
+  if (want("c5+rec")) report<C5R>(x, out, st);
+  if (want("sq+rec")) report<SQR>(x, out, st);
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
   return 0;
