@@ -7,13 +7,22 @@
 // Cuthill-McKee ordering of it (converter.m:14-15, symrcm; hspmv_rcm_reorder,
 // whose tie-breaking is not Octave's).  converter.m walks a directory
 // (~/matrices/mm/*.mtx -> norm/X.mtx.csr and rcm/X.mtx.rcm.csr); a shell
-// loop over this tool does the same.  Host only.
+// loop over this tool does the same.  An output named *.bin is written as
+// the binary cache instead of text (hspmv_save_bin).  Host only.
 #include <stdio.h>
 #include <string.h>
 
 #include <chrono>
 
 #include "hspmv.h"
+
+// ".bin" outputs get the binary cache (hspmv_save_bin: what spmv-csr /
+// spmv-csrk load fastest), anything else the reference's text .csr
+static int write_out(const char *path, const hspmv_csr *A) {
+  const size_t n = strlen(path);
+  if (n >= 4 && strcmp(path + n - 4, ".bin") == 0) return hspmv_save_bin(path, A, nullptr);
+  return hspmv_write_csr(path, A);
+}
 
 static int die(const char *what) {
   fprintf(stderr, "%s failed: %s\n", what, hspmv_last_error());
@@ -44,7 +53,7 @@ int main(int argc, char **argv) {
     }
     printf("reordered in %f...", std::chrono::duration<double>(std::chrono::steady_clock::now() - tic).count());
   }
-  if (hspmv_write_csr(argv[2], &view) != HSPMV_OK) {
+  if (write_out(argv[2], &view) != HSPMV_OK) {
     hspmv_free_csr(&R);
     hspmv_free_csr(&A);
     return die("\nwrite");
@@ -53,7 +62,7 @@ int main(int argc, char **argv) {
   int rc = 0;
   if (rcm) {
     const hspmv_csr rv = {R.m, R.n, R.nnz, R.row_ptr, R.col_idx, R.val, R.dtype};
-    if (hspmv_write_csr(argv[3], &rv) != HSPMV_OK)
+    if (write_out(argv[3], &rv) != HSPMV_OK)
       rc = die("\nwrite");
     else
       printf("converted reordered to csr...wrote row_ptr...wrote col_ind...wrote val...");

@@ -177,3 +177,14 @@ def test_rcm_reorder_is_a_symmetric_permutation_that_narrows_the_band():
     assert np.array_equal(np.sort(p2), np.arange(5)) and R2.nnz == 4
     with pytest.raises(hspmv.HspmvError):
         hspmv.rcm_reorder(hspmv.CsrMatrix(2, 3, np.array([0, 1, 1]), np.array([2]), np.ones(1)))
+
+
+def test_mtx2csr_binary_outputs(tmp_path):
+    f = tmp_path / "sym.mtx"
+    f.write_text(MTX["symmetric_real"])
+    run(BUILD / "mtx2csr", f, tmp_path / "s.bin", tmp_path / "s.rcm.bin")
+    A, maps = hspmv.load_bin(tmp_path / "s.bin")
+    S = expected(f)
+    assert maps is None and np.array_equal(A.row_ptr, S.indptr) and np.array_equal(A.val, S.data)
+    R, _ = hspmv.load_bin(tmp_path / "s.rcm.bin")
+    assert R.nnz == S.nnz
