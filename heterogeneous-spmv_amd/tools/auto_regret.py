@@ -47,7 +47,11 @@ def _rows_random(m: int, n: int, k: int, seed: int, dtype=np.float64) -> hspmv.C
 
 
 def build(name: str):
-    """(A, maps, description) of one zoo matrix."""
+    """(A, maps, description) of one zoo matrix (suffix ":f32": in fp32, the
+    reference's own value type)."""
+    if name.endswith(":f32"):
+        A, maps, desc = build(name[:-4])
+        return A.astype(np.float32), maps, desc + " [fp32]"
     if name in BASE:
         import sweep
         return sweep.build(name)
