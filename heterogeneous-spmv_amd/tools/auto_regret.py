@@ -126,8 +126,12 @@ def main():
         t0 = time.time()
         A, maps, desc = build(name)
         x = gen.rand_x(A.n, 42).astype(A.val.dtype)
-        y_ref = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
-        absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+        # fp64 sums of the (fp32 or fp64) data; fp32 y may differ from them by
+        # its own summation error, bounded by (row length + 2) fp32 ulps of
+        # sum |a x| (tests/test_gpu_parity.py's fp32 bar)
+        y_ref = oracle.spmv(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
+        absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
+        rowlen = np.diff(A.row_ptr).astype(np.float64)
         print(f"# {name}: {desc} m={A.m} n={A.n} nnz={A.nnz} built in {time.time() - t0:.1f}s",
               file=sys.stderr, flush=True)
         dev = sweep.DeviceMatrix(A, x)
@@ -144,7 +148,8 @@ def main():
             op.synchronize()
             y = dev.y.cpu().numpy().astype(np.float64)
             f64 = A.val.dtype == np.float64
-            tol = (1e-6 if f64 else 1e-4) * np.abs(y_ref) + (1e-12 if f64 else 1e-5) * absrow
+            tol = (1e-6 * np.abs(y_ref) + 1e-12 * absrow if f64
+                   else (rowlen + 2) * 2.0 ** -23 * absrow + 1e-30)
             ok = bool(np.all(np.abs(y - y_ref) <= tol))
             ops.append((vname, op, ok))
         times = {v: [] for v, _, _ in ops}
