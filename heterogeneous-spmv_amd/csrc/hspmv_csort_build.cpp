@@ -24,8 +24,8 @@ namespace hspmv {
 // padded to whole chunks of 64*U, and a chunk is closed early when its
 // columns would span more than 65535 (16-bit offsets from the chunk base).
 // Padding entries add 0 * x[base] to a dummy slot that is never read.
-// Auto: HBM-resident matrices with irregular gathers and x beyond an XCD's
-// L2 (the x-slab rule, which it replaces: C5 264 -> ~110 us), unless the
+// Auto: HBM-resident matrices with irregular gathers from an x beyond the
+// L1 (> 256 KiB; it replaced the x-slab rule: C5 264 -> ~110 us), unless the
 // handle asks for deterministic sums (the slots add in atomic order);
 // HSPMV_KERNEL_CSORT forces it, Tuning.csort = -1 turns auto off,
 // Tuning.csort_parts = 1/2/4 sets the column parts, csort_u = 4/8/16 the

@@ -570,8 +570,14 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
     // a deterministic handle never builds the csort tables: the planner
     // would pick kCsort whenever they exist (plan_launch)
     bool want = !s.tune.deterministic && (kf == kCsort || cm == 1);
+    // Scattered gathers from an x the L1 cannot hold go to the L2 one line
+    // per nonzero, at its request rate, whatever the L2's capacity: until r04
+    // the rule also asked for x beyond an XCD's 4 MiB L2, which kept fp32
+    // `mix` (x = 3.8 MiB, random columns within +-4000) on the CSR3 kernel
+    // at 90.8 us against csort's 62.5 (profiles/r04/auto_regret_f32.jsonl);
+    // x of a few L1s (the zoo's `tall`, 16-32 KiB) stays on the row kernels.
     if (!want && kf == kAuto && cm == 0 && !s.tune.deterministic && s.tune.x_slabs == 0 &&
-        footprint > kMallResident && (double)n * sv > 4.0 * 1024 * 1024)
+        footprint > kMallResident && (double)n * sv > 256.0 * 1024)
       want = irregular_gathers(rp, col, m, sv);
     if (want) {
       if ((rc = build_csort(s, rp, col, val, m, n, dtype, flags))) return rc;
