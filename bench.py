@@ -2,7 +2,10 @@
 """bench.py -- SpMV GFLOP/s and achieved HBM GB/s (fp64) on 1..8 MI355X.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
-launched with torch.distributed.run, one rank per GPU.  A "step" is one SpMV
+launched with torch.distributed.run, one rank per GPU -- or, when no launcher
+set WORLD_SIZE, bench.py starts that launcher itself as a child process (the
+parent touches no GPU, relays rank 0's line and exits with the child's code;
+``self_launch``).  A "step" is one SpMV
 y = A x over every rank's row-range shard of the workload (inputs resident in
 HBM; no data-path collective -- rows are independent).
 W untimed steps, then exactly K steps bracketed by barrier + synchronize; the
@@ -53,6 +56,12 @@ Extra fields on the line:
                domain, matrix first-touched per thread; beside it
                reference_f32: the reference's own omp_spmv (spmv-csr/spmv.c,
                built unmodified into oracle/_ref) on the fp32 copy
+  cpu_c1       BASELINE configs[0] itself: the same OpenMP restatement on the
+               1000 x 1000 5-point Laplacian (m = 1e6, nnz = 4,996,000) in
+               fp64, x = 1 (the reference CLI's x) and x = rand:42, under
+               OMP_SCHEDULE static and guided (run_norm.py:18,65-66,
+               run_cuda_new.py:79), 5 warm-ups + timed runs, TimeMin / TimeMax
+               / TimeAvg and GFLOP/s from TimeMin (rank 0 at N = 1 only)
 """
 from __future__ import annotations
 
@@ -214,7 +223,7 @@ def load_traffic(workload_key: str):
 CPU_WAIT_POLICY = None
 
 
-def cpu_baseline(A, x, budget_s: float):
+def cpu_baseline(A, x, budget_s: float, extra_args=()):
     """The CPU legs (oracle/cpu_bench.py: the oracle's omp_spmv restatement,
     spmv-csr/spmv.c:92-114, and the reference's own omp_spmv in fp32) on the
     SAME matrix, in a process of their own: the matrix and x go through a
@@ -235,13 +244,42 @@ def cpu_baseline(A, x, budget_s: float):
         if CPU_WAIT_POLICY:
             env["OMP_WAIT_POLICY"] = CPU_WAIT_POLICY
         out = subprocess.run([sys.executable, str(REPO / "oracle" / "cpu_bench.py"), "--dir", str(d),
-                              "--budget", str(budget_s)], env=env, capture_output=True, text=True,
-                             timeout=600)
+                              "--budget", str(budget_s), *extra_args], env=env, capture_output=True,
+                             text=True, timeout=600)
         if out.returncode != 0:
             raise RuntimeError(f"oracle/cpu_bench.py failed: {out.stderr[-1500:]}")
         return json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     finally:
         shutil.rmtree(d, ignore_errors=True)
+
+
+def cpu_c1(budget_s: float) -> dict:
+    """BASELINE configs[0]: spmv-csr's OpenMP loop (the oracle's omp_spmv
+    restatement, oracle/cpu_bench.py) on the 1000 x 1000 5-point Laplacian in
+    fp64 on this box's host cores.  Both x the reference CLI knows of -- x = 1
+    (spmv-csr/spmv.c:133) and a seeded x = rand:42 -- each under
+    OMP_SCHEDULE static and guided (run_norm.py:18,65-66; run_cuda_new.py:79),
+    5 warm-ups + timed runs around each call (spmv.c:164-185); TimeMin /
+    TimeMax / TimeAvg in seconds and GFLOP/s = 2 nnz / TimeMin."""
+    from hspmv import gen
+    A = gen.laplace2d(1000, 1000)
+    legs, first = {}, None
+    for name, x in (("ones", np.ones(A.n)), ("rand:42", gen.rand_x(A.n, 42))):
+        c = cpu_baseline(A, x, budget_s, ("--no-tried", "--no-reference"))
+        first = first or c
+        legs[name] = {
+            sched: {"TimeMin": leg["time_min_s"], "TimeMax": leg["time_max_s"],
+                    "TimeAvg": leg["time_avg_s"], "gflops": round(2.0 * A.nnz / leg["time_min_s"] * 1e-9, 3),
+                    "runs": leg["runs"]}
+            for sched, leg in (("static", dict(c, runs=c["guided"]["runs"])), ("guided", c["guided"]))}
+    return {"config": "c1: spmv-csr OpenMP fp64, 5-pt Laplacian 1000 x 1000", "m": A.m, "nnz": A.nnz,
+            "dtype": "f64", "kind": "port", "cores": first["cores"], "cores_note": first["cores_note"],
+            "cgroup_cpu_quota": first["cgroup_cpu_quota"], "x": legs,
+            "value": legs["rand:42"]["static"]["gflops"], "unit": "GFLOP/s",
+            "sample": (f"gen.laplace2d(1000, 1000): m={A.m}, nnz={A.nnz}, fp64 CSR; omp_spmv restatement "
+                       f"(oracle/spmv_oracle.c), {first['cores']} threads, 5 warm-ups + "
+                       f"{first['guided']['runs']} timed runs per (x, schedule); value = x rand:42, "
+                       f"static, 2 nnz / TimeMin")}
 
 
 def single_gpu_point(args, stream, cfg: str):
@@ -423,11 +461,51 @@ def overlapped_gather(args, A, shard, x, y, stream, device, info, world, chunks:
 
 # ------------------------------------------------------------------ main
 
+# Environment the ranks of a self-launched run get when the caller left it
+# unset.  HSA_ENABLE_IPC_MODE_LEGACY=0: the box's driver only supports dmabuf
+# IPC, and RCCL's peer setup fails with hipIpcGetMemHandle: invalid argument
+# without it.
+RANK_ENV = {"HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+
+
+def launch_command(argv, gpus: int, port: int) -> list:
+    """torch.distributed.run over this script with the same arguments: one
+    rank per GPU of this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()),
+            *argv]
+
+
+def self_launch(args, argv) -> int:
+    """``bench.py --gpus N`` (N > 1) with no launcher around it: start the
+    launcher as a CHILD process (never exec: this process must not replace
+    itself, and it touches no GPU -- torch is not even imported here), relay
+    the ranks' stdout (rank 0's one JSON line), return the child's exit code.
+    The reference's harness runs its binaries directly (run_norm.py:73-76);
+    this keeps the same one-command shape for the N-GPU runs."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    for k, v in RANK_ENV.items():
+        env.setdefault(k, v)
+    proc = subprocess.Popen(launch_command(argv, args.gpus, port), env=env, stdout=subprocess.PIPE,
+                            text=True, bufsize=1)
+    for line in proc.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return proc.wait()
+
+
 def main():
     args = parse()
     if args.dry_run:
         dry_run(args)
         return
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args, sys.argv[1:]))
     import torch  # device memory, streams, torch.distributed: plumbing
 
     import hspmv
@@ -570,9 +648,10 @@ def main():
             scal = strong_scaling(n1, world, flops_step / step_s * 1e-9, cold_g)
         ok_all = reduce_over_ranks(1.0 if ok_all else 0.0, world, "sum") == world
 
-    cpu = None
+    cpu = c1 = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(A, x_host, args.cpu_seconds)
+        c1 = cpu_c1(max(0.2, 0.25 * args.cpu_seconds))
 
     if rank == 0:
         ctype = "double" if np_dt == np.float64 else "float"
@@ -646,6 +725,7 @@ def main():
             "scaling_reference": sref,
             "strong_scaling": scal,
             "cpu_baseline": cpu,
+            "cpu_c1": c1,
         }
         print(json.dumps(out), flush=True)
     op.close()

@@ -378,11 +378,14 @@ hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
   if (e != hipSuccess || c.direct) return e;
   // rows per finishing thread: 4 (32-byte partial loads; C5 104.4 -> 103.5
   // us, c5r 110.0 -> 107.8 against 2, r04c/ab_c5_fin_rows.jsonl), fewer when
-  // m is not a multiple; c.fin_rows overrides (A/B)
+  // m is not a multiple or y (a caller's buffer, hspmv_bind_y_device: any
+  // element-aligned pointer) is not aligned for the R-wide vector store;
+  // c.fin_rows overrides (A/B)
   const int fr = c.fin_rows > 0 ? c.fin_rows : 4;
-  if (fr >= 4 && c.m % 4 == 0)
+  const uintptr_t ya = reinterpret_cast<uintptr_t>(y);
+  if (fr >= 4 && c.m % 4 == 0 && ya % (4 * sizeof(T)) == 0)
     launch_finish<T, S, 4>(c, part, spart, y, st);
-  else if (fr >= 2 && c.m % 2 == 0)
+  else if (fr >= 2 && c.m % 2 == 0 && ya % (2 * sizeof(T)) == 0)
     launch_finish<T, S, 2>(c, part, spart, y, st);
   else
     launch_finish<T, S, 1>(c, part, spart, y, st);

@@ -441,11 +441,8 @@ extern "C" {
 
 int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   clear_error();
-  hspmv_info full;
-  int rc = fill_info(h, &full);
-  if (rc) return rc;
-  memcpy(out, &full, offsetof(hspmv_info, deterministic));  // the 0.1 layout
-  return HSPMV_OK;
+  if (!out) return set_error(HSPMV_E_INVALID, "NULL output");
+  return fill_info(h, out);
 }
 
 #ifdef HSPMV_ENV_KNOBS

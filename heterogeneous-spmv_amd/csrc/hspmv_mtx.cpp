@@ -43,8 +43,10 @@ struct Entry {
 
 inline bool blank(char ch) { return ch == ' ' || ch == '\t' || ch == '\r'; }
 
-// One entry line [p, e): "i j [v]" (1-based).  Returns false if malformed.
-bool parse_line(const char *p, const char *e, bool pattern, Entry *out) {
+// One entry line [p, e): "i j [v]" (1-based).  Returns false if malformed or
+// if an index lies outside 1..rows / 1..cols (checked on the 64-bit values,
+// before narrowing to int32: 4294967297 must not wrap to row 0).
+bool parse_line(const char *p, const char *e, bool pattern, long long rows, long long cols, Entry *out) {
   long long ij[2];
   for (int t = 0; t < 2; ++t) {
     while (p < e && blank(*p)) ++p;
@@ -52,11 +54,22 @@ bool parse_line(const char *p, const char *e, bool pattern, Entry *out) {
     if (r.ec != std::errc()) return false;
     p = r.ptr;
   }
+  if (ij[0] < 1 || ij[0] > rows || ij[1] < 1 || ij[1] > cols) return false;
   double v = 1.0;
   if (!pattern) {
     while (p < e && blank(*p)) ++p;
     auto r = std::from_chars(p, e, v);
-    if (r.ec != std::errc() && r.ec != std::errc::result_out_of_range) return false;
+    if (r.ec == std::errc::result_out_of_range) {
+      // from_chars leaves v unset here; strtod gives what mmread's fscanf
+      // gives: +-HUGE_VAL on overflow, a denormal or +-0 on underflow
+      char tok[128];
+      const size_t n = std::min<size_t>((size_t)(r.ptr - p), sizeof(tok) - 1);
+      memcpy(tok, p, n);
+      tok[n] = 0;
+      v = strtod(tok, nullptr);
+    } else if (r.ec != std::errc()) {
+      return false;
+    }
   }
   out->r = (int32_t)(ij[0] - 1);
   out->c = (int32_t)(ij[1] - 1);
@@ -151,7 +164,7 @@ extern "C" int hspmv_read_mtx(const char *path, int dtype, hspmv_csr_buf *out) {
           while (s < l && blank(*s)) ++s;
           if (s < l && *s != '%') {
             Entry en;
-            if (!parse_line(s, l, pattern, &en) || en.r < 0 || en.r >= rows || en.c < 0 || en.c >= cols) {
+            if (!parse_line(s, l, pattern, rows, cols, &en)) {
               bad[(size_t)t] = 1;
               return;
             }

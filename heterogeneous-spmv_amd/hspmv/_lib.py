@@ -1,6 +1,6 @@
 """ctypes binding of libhspmv.so (the C ABI declared in include/hspmv.h).
 
-The library is loaded from ``heterogeneous-spmv_amd/build/libhspmv.so`` (built
+The library is loaded from ``heterogeneous-spmv_amd/build/libhspmv.so.1`` (built
 in-tree by ``make`` / ``__graft_entry__.build()``).  There is no fallback: if
 the shared library is missing or fails to load, :func:`lib` raises.
 """
@@ -12,7 +12,7 @@ from pathlib import Path
 
 PKG_ROOT = Path(__file__).resolve().parent.parent          # heterogeneous-spmv_amd/
 REPO_ROOT = PKG_ROOT.parent
-LIB_PATH = Path(os.environ.get("HSPMV_LIB", PKG_ROOT / "build" / "libhspmv.so"))
+LIB_PATH = Path(os.environ.get("HSPMV_LIB", PKG_ROOT / "build" / "libhspmv.so.1"))
 HEADER = REPO_ROOT / "include" / "hspmv.h"
 
 F32, F64 = 0, 1

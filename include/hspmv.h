@@ -34,12 +34,17 @@
 extern "C" {
 #endif
 
-#define HSPMV_VERSION_MAJOR 0
-#define HSPMV_VERSION_MINOR 3  /* 0.2: hspmv_options, info.deterministic;
-                                  0.3: info.rccl_version / csort chunks,
-                                  hspmv_get_info fills the 0.1 layout only,
-                                  hspmv_xdict_plan_ex, hspmv_rccl_version,
-                                  hspmv_read_mtx, hspmv_rcm_reorder */
+/* ABI history.  0.2: hspmv_options, info.deterministic.  0.3: info.rccl_version
+ * / csort chunks, hspmv_xdict_plan_ex, hspmv_rccl_version, hspmv_read_mtx,
+ * hspmv_rcm_reorder -- and two changes a 0.2 binary could not see
+ * (hspmv_xdict_plan's 3rd argument became kernel flags; hspmv_get_info's
+ * layout shrank).  1.0 declares that break: the library is libhspmv.so.1
+ * (SONAME), so a binary built against 0.x fails to load instead of
+ * misreading arguments; hspmv_get_info fills the whole 1.0 hspmv_info.
+ * Within a major, structs only grow at the end (hspmv_options.struct_size,
+ * hspmv_get_info_sized) and signatures never change. */
+#define HSPMV_VERSION_MAJOR 1
+#define HSPMV_VERSION_MINOR 0
 
 /* ---------------------------------------------------------------- status */
 #define HSPMV_OK 0
@@ -362,9 +367,8 @@ int hspmv_get_y(hspmv_handle *h, void *y_host);
  * every GPU's full-length buffer, timed (seconds).  Either pointer may be NULL. */
 int hspmv_exchange(hspmv_handle *h, double *bcast_x_s, double *gather_y_s);
 
-/* Fills the 0.1 layout of hspmv_info only (every field before
- * `deterministic`), so a caller built against any header gets no write past
- * its struct.  The fields since 0.2 come from hspmv_get_info_sized. */
+/* Fills the whole hspmv_info of this major (1.x callers; NULL -> E_INVALID).
+ * A caller built against an older 1.x header uses hspmv_get_info_sized. */
 int hspmv_get_info(hspmv_handle *h, hspmv_info *out);
 /* Fills min(out_size, sizeof(hspmv_info)) bytes: pass sizeof(hspmv_info) of
  * the header you were built against. */
@@ -465,8 +469,8 @@ int hspmv_partition_rows(int64_t m, const int32_t *row_ptr,
 int hspmv_xdict_plan_ex(const hspmv_csr *A, const hspmv_csr3_maps *maps, const hspmv_options *opt,
                         int64_t cap_entries, int64_t *n_blocks, int64_t *n_records,
                         int32_t *blk, int32_t *runs, uint16_t *pos);
-/* The 0.1 form: kernel flags instead of options (= hspmv_xdict_plan_ex with
- * an hspmv_options holding only these flags). */
+/* Kernel flags instead of options (= hspmv_xdict_plan_ex with an
+ * hspmv_options holding only these flags). */
 int hspmv_xdict_plan(const hspmv_csr *A, const hspmv_csr3_maps *maps, unsigned flags,
                      int64_t cap_entries, int64_t *n_blocks, int64_t *n_records,
                      int32_t *blk, int32_t *runs, uint16_t *pos);

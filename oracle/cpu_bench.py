@@ -219,6 +219,8 @@ def run(d: Path, budget_s: float, threads: int = 0, bind: bool = True, tried: bo
                       "gflops_from_median": res["guided"]["gflops_from_median"],
                       "gflops_from_avg": res["guided"]["gflops_from_avg"],
                       "time_min_s": res["guided"]["time_min_s"],
+                      "time_max_s": res["guided"]["time_max_s"],
+                      "time_avg_s": res["guided"]["time_avg_s"],
                       "median_s": res["guided"]["median_s"], "runs": runs}}
     if reference:
         v32 = np.ascontiguousarray(val, np.float32)

@@ -102,11 +102,50 @@ def test_rccl_version_is_the_resolved_librccl():
     assert "rccl_version" in dict(_lib.Info._fields_)
 
 
-def test_get_info_fills_only_the_0_1_layout():
-    """hspmv_get_info never writes past the 0.1 struct (fields before
-    `deterministic`), so an old caller cannot be overrun; the newer fields
-    come from hspmv_get_info_sized.  Checked on the header offsets."""
+def test_abi_major_is_in_the_soname():
+    """ABI 1.0 declares 0.3's incompatible changes (hspmv_xdict_plan's third
+    argument, hspmv_get_info's layout) by the major version: the library is
+    libhspmv.so.1 and its SONAME says so, so a binary linked against 0.x
+    (NEEDED libhspmv.so) does not load it and misread arguments."""
     text = _lib.HEADER.read_text()
-    assert "#define HSPMV_VERSION_MINOR 3" in text
-    assert _lib.Info.deterministic.offset < ctypes.sizeof(_lib.Info)
-    assert _lib.Info.rccl_version.offset > _lib.Info.csort_row_blocks.offset
+    assert "#define HSPMV_VERSION_MAJOR 1" in text and "#define HSPMV_VERSION_MINOR 0" in text
+    assert _lib.LIB_PATH.name == "libhspmv.so.1"
+    out = subprocess.run(["readelf", "-d", str(_lib.LIB_PATH)], capture_output=True, text=True)
+    assert out.returncode == 0 and "Library soname: [libhspmv.so.1]" in out.stdout
+    assert hspmv.version().startswith("hspmv 1.0")
+    cli = _lib.PKG_ROOT / "build" / "spmv-csr"
+    out = subprocess.run(["readelf", "-d", str(cli)], capture_output=True, text=True)
+    assert "Shared library: [libhspmv.so.1]" in out.stdout
+
+
+def test_get_info_rejects_null_without_a_handle():
+    """hspmv_get_info / hspmv_get_info_sized with NULL arguments return
+    HSPMV_E_INVALID (no GPU: the handle-free paths only; the NULL-output
+    case on a live handle is test_get_info_null_output_and_canary)."""
+    L = hspmv.lib()
+    assert L.hspmv_get_info(None, None) == -1
+    assert L.hspmv_get_info_sized(None, None, 16) == -1
+    assert L.hspmv_last_error()
+
+
+@pytest.mark.gpu
+def test_get_info_null_output_and_canary():
+    """On a live handle: hspmv_get_info(h, NULL) is HSPMV_E_INVALID (it
+    used to dereference NULL); hspmv_get_info_sized with the 0.1-sized
+    prefix writes exactly that many bytes -- a canary after it survives --
+    and agrees with the full report on those bytes."""
+    from hspmv import gen
+    L = hspmv.lib()
+    A = gen.laplace2d(30, 20)
+    with hspmv.SpMV(A, device=0) as op:
+        h = op._h
+        assert L.hspmv_get_info(h, None) == -1 and b"NULL" in L.hspmv_last_error()
+        full = _lib.Info()
+        assert L.hspmv_get_info(h, ctypes.byref(full)) == 0 and full.num_gpus == 1
+        n01 = _lib.Info.deterministic.offset
+        buf = (ctypes.c_ubyte * (ctypes.sizeof(_lib.Info) + 64))()
+        for i in range(len(buf)):
+            buf[i] = 0xA5
+        assert L.hspmv_get_info_sized(h, ctypes.cast(buf, ctypes.POINTER(_lib.Info)), n01) == 0
+        assert all(buf[i] == 0xA5 for i in range(n01, len(buf)))
+        assert bytes(buf[:n01]) == bytes(memoryview(full).cast("B")[:n01])

@@ -67,6 +67,66 @@ def test_c3_shards_cover_the_matrix_on_ssr_boundaries():
         assert rows == A.m
 
 
+_SPAWN_PROBE = r"""
+import json, subprocess, sys
+sys.argv = ["bench.py", "--gpus", "4", "--steps", "7"]
+seen = {}
+class FakeProc:
+    def __init__(self, cmd, **kw):
+        seen["cmd"] = cmd
+        seen["env_ipc"] = kw["env"].get("HSA_ENABLE_IPC_MODE_LEGACY")
+        seen["torch_loaded"] = sorted(m for m in sys.modules if m == "torch" or m.startswith("torch."))
+        seen["hspmv_loaded"] = sorted(m for m in sys.modules if m.startswith("hspmv"))
+        self.stdout = iter(['{"value": 1.0}\n'])
+    def wait(self):
+        return 5
+subprocess.Popen = FakeProc
+import bench
+try:
+    bench.main()
+except SystemExit as e:
+    seen["exit"] = e.code
+print("PROBE " + json.dumps(seen))
+"""
+
+
+def test_self_launch_spawns_the_launcher_without_touching_the_gpu():
+    """`python bench.py --gpus N` with no WORLD_SIZE: the parent starts
+    torch.distributed.run over itself as a child (same arguments, 127.0.0.1
+    rendezvous, the RCCL IPC environment), relays its stdout and exits with
+    its code -- and has imported neither torch (so no torch.cuda) nor the
+    HIP library when it spawns."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "HSA_ENABLE_IPC_MODE_LEGACY")}
+    out = subprocess.run([sys.executable, "-c", _SPAWN_PROBE], cwd=REPO, env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert '{"value": 1.0}' in out.stdout  # relayed
+    seen = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("PROBE ")][0][6:])
+    assert seen["torch_loaded"] == [] and seen["hspmv_loaded"] == []
+    assert seen["exit"] == 5 and seen["env_ipc"] == "0"
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "7"] and cmd[-5].endswith("bench.py")
+
+
+def test_cpu_c1_leg_times_configs0(monkeypatch):
+    """The cpu_c1 leg: configs[0]'s matrix (nnz = 4,996,000), fp64, x = 1 and
+    x = rand:42, static and guided, TimeMin/Max/Avg and GFLOP/s from TimeMin."""
+    sys.path.insert(0, str(REPO))
+    import bench
+    c = bench.cpu_c1(0.2)
+    assert c["m"] == 1_000_000 and c["nnz"] == 4_996_000 and "nnz=4996000" in c["sample"]
+    assert c["dtype"] == "f64" and c["kind"] == "port" and c["cores"] >= 1
+    for xname in ("ones", "rand:42"):
+        for sched in ("static", "guided"):
+            leg = c["x"][xname][sched]
+            assert 0 < leg["TimeMin"] <= leg["TimeAvg"] <= leg["TimeMax"]
+            assert abs(leg["gflops"] - 2 * c["nnz"] / leg["TimeMin"] * 1e-9) < 1e-2
+    assert c["value"] == c["x"]["rand:42"]["static"]["gflops"]
+
+
 def test_cpu_baseline_runs_in_its_own_process(tmp_path):
     """bench.py's CPU legs (oracle/cpu_bench.py) on a small matrix: a process
     of its own, the reference protocol's min / median / avg, the reported
@@ -131,6 +191,12 @@ def test_bench_json_line_contract():
     assert d["strong_scaling"] is None  # N = 1: scaling_reference instead
     assert abs(c["value"] - 2 * d["config"]["nnz"] / c["time_min_s"] * 1e-9) < 1e-2 * c["value"]
     assert "nnz=51895117" in c["sample"]
+    c1 = d["cpu_c1"]  # configs[0] itself on this host
+    assert c1["nnz"] == 4_996_000 and "nnz=4996000" in c1["sample"] and c1["dtype"] == "f64"
+    for xname in ("ones", "rand:42"):
+        for sched in ("static", "guided"):
+            leg = c1["x"][xname][sched]
+            assert 0 < leg["TimeMin"] <= leg["TimeAvg"] <= leg["TimeMax"] and leg["gflops"] > 0
     ref = c["reference_f32"]  # the reference's own omp_spmv, when oracle/_ref was built
     if (REPO / "oracle" / "_ref" / "libref_spmvcsr.so").exists():
         assert ref["kind"] == "reference" and ref["value"] > 0 and ref["time_min_s"] > 0
@@ -143,20 +209,16 @@ def test_bench_json_line_contract():
 
 @pytest.mark.gpu
 def test_bench_multi_rank_path_rehearsal_on_one_gpu(tmp_path):
-    """bench.py's N > 1 code path (shards, x broadcast, barriers, max over
-    ranks, y all-gather, halo exchange, rank-0 JSON line) run as 2 ranks that
+    """bench.py's N > 1 code path (self-launched ranks, shards, x broadcast,
+    barriers, max over ranks, y all-gather, halo exchange, rank-0 JSON line)
+    run as 2 ranks that
     share device 0 and exchange over gloo -- RCCL allows one rank per device,
     so this is the rehearsal a one-GPU box can do; the driver's N > 1 runs use
     RCCL on one GPU per rank.  C2 (weak scaling) keeps it short."""
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    env = dict(os.environ, PYTHONUNBUFFERED="1")
-    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-                          "--master-port", str(port), str(REPO / "bench.py"), "--gpus", "2",
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONUNBUFFERED"] = "1"
+    # the plain command: bench.py starts its own launcher (self_launch)
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2",
                           "--backend", "gloo", "--same-device", "--config", "c2",
                           "--steps", "10", "--warmup", "2", "--cold-steps", "2"],
                          cwd=REPO, env=env, capture_output=True, text=True, timeout=400)

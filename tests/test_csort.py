@@ -104,6 +104,32 @@ def test_csort_chunk_sizes(u, dtype):
     check(A, x, y)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_csort_caller_y_at_any_element_offset(dtype):
+    """hspmv_bind_y_device takes any element-aligned pointer: the finishing
+    pass's 4- and 2-row vector stores are used only when y is aligned for
+    them (csort.hip launch_csort_u), so a torch slice at offset 1..3 and an
+    m that is not a multiple of 4 give the right y, and the elements on
+    either side of the bound range keep their canary."""
+    import torch
+    for m in (40_000, 40_001, 40_002):
+        A = gen.powerlaw(m, seed=4, dtype=dtype)
+        x = gen.rand_x(A.n, 6).astype(dtype)
+        tdt = torch.float32 if dtype == np.float32 else torch.float64
+        xd = torch.from_numpy(x).to("cuda")
+        for off in (0, 1, 2, 3):
+            buf = torch.full((A.m + 8,), 7.0, dtype=tdt, device="cuda")
+            with hspmv.SpMV(A, kernel="csort", options={"csort_parts": 2}) as op:
+                assert op.info["kernel_name"] == "csort"
+                op.bind_x_device(xd.data_ptr())
+                op.bind_y_device(buf.data_ptr() + off * buf.element_size())
+                op.spmv()
+                torch.cuda.synchronize()
+            h = buf.cpu().numpy()
+            assert np.all(h[:off] == 7.0) and np.all(h[off + A.m:] == 7.0), (m, off)
+            check(A, x, h[off:off + A.m])
+
+
 def test_csort_long_rows_whole_and_sliced():
     A = _long_rows(seed=8)
     x = gen.rand_x(A.n, 2)

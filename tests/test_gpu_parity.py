@@ -3,7 +3,8 @@
 Bar (BASELINE.json north star): fp64 y within
     |y - y64| <= 1e-6 |y64| + 1e-12 * sum_k |a_k x_k|
 of the spmv-csr restatement.  The STREAM / CSR3 kernels sum each row in the
-reference order with the reference rounding, so on rows up to 32 nonzeros
+reference order with the reference rounding, so on rows up to 40 nonzeros
+(SERIAL_MAX, spmv_device.cuh kSerialMax)
 they are checked BITWISE: fp32 against the reference binary's own golden
 output, fp64 against the restatement.
 """
@@ -48,7 +49,7 @@ def short_rows(A):
 
 def test_golden_fp32_bitwise_vs_reference_binary(golden_names):
     """STREAM / CSR3 in fp32 reproduce the reference's own omp_spmv output
-    bit for bit on every row of up to 32 nonzeros (x = 1 and x = rand)."""
+    bit for bit on every row of up to 40 nonzeros (x = 1 and x = rand)."""
     for name in golden_names:
         A = hspmv.read_csr(GOLDEN / f"{name}.csr", np.float32)
         g = load_golden(name)
@@ -612,7 +613,7 @@ def _slab_exact_rows(A, slabs):
 def test_xslabs_bitwise_rows_and_fallback():
     """x slabs (options x_slabs=B forces B column slabs): the row kernel runs
     once per slab over a slab-major copy, each pass continuing the rows
-    from y.  Rows whose slab segments are all <= 32 nonzeros are
+    from y.  Rows whose slab segments are all <= 40 nonzeros are
     bit-identical to the oracle (fp64 restatement, fp32 reference loop),
     the rest within the fp64 bar; split rows, empty rows, CSR3 tasks,
     prefetch and U = 2 included.  Unsorted rows fall back (x_slabs = 0)."""

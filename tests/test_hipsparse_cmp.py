@@ -57,7 +57,7 @@ def test_hipsparse_comparison_full_configs(cfgs, tmp_path):
         x = _x(A.n, A.val.dtype)
         h = recs[0]
         yh = np.fromfile(tmp_path / f"{cfg}_hspmv.bin", A.val.dtype)
-        exact = np.diff(A.row_ptr) <= 32 if h["kernel"] in ("stream", "csr3") else None
+        exact = np.diff(A.row_ptr) <= 40 if h["kernel"] in ("stream", "csr3") else None
         _check(A, x, yh, exact)
         for r in recs[1:]:
             if "t_min_us" not in r:

@@ -99,6 +99,9 @@ def test_read_mtx_errors(tmp_path):
         "complex.mtx": "%%MatrixMarket matrix coordinate complex general\n1 1 1\n1 1 1 0\n",
         "short.mtx": "%%MatrixMarket matrix coordinate real general\n2 2 3\n1 1 1\n2 2 1\n",
         "range.mtx": "%%MatrixMarket matrix coordinate real general\n2 2 1\n3 1 1\n",
+        # 2^32 + 1 would wrap to row 1 if narrowed to int32 before the check
+        "wrap.mtx": "%%MatrixMarket matrix coordinate real general\n2 2 1\n4294967297 1 1\n",
+        "zero_index.mtx": "%%MatrixMarket matrix coordinate real general\n2 2 1\n1 0 1\n",
         "nonsquare_sym.mtx": "%%MatrixMarket matrix coordinate real symmetric\n2 3 1\n1 1 1\n",
         "noheader.mtx": "2 2 1\n1 1 1\n",
     }
@@ -109,6 +112,20 @@ def test_read_mtx_errors(tmp_path):
             hspmv.read_mtx(f)
     with pytest.raises(hspmv.HspmvError):
         hspmv.read_mtx(tmp_path / "missing.mtx")
+
+
+def test_read_mtx_out_of_range_values(tmp_path):
+    """Values beyond the double range read as mmread's fscanf reads them:
+    1e400 -> +Inf, -1e400 -> -Inf, 1e-400 -> 0 (then dropped as an explicit
+    zero), never as the parser's initial 1.0."""
+    f = tmp_path / "huge.mtx"
+    f.write_text("%%MatrixMarket matrix coordinate real general\n3 3 4\n"
+                 "1 1 1e400\n2 2 -1e400\n3 3 1e-400\n1 3 2.5\n")
+    A = hspmv.read_mtx(f, np.float64)
+    d = {(r, int(c)): v for r in range(A.m)
+         for c, v in zip(A.col_idx[A.row_ptr[r]:A.row_ptr[r + 1]], A.val[A.row_ptr[r]:A.row_ptr[r + 1]])}
+    assert d[(0, 0)] == np.inf and d[(1, 1)] == -np.inf and d[(0, 2)] == 2.5
+    assert (2, 2) not in d and A.nnz == 3
 
 
 def test_read_mtx_large_parallel(tmp_path):

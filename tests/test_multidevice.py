@@ -10,14 +10,13 @@ repeated devices and gloo (tests/test_sharded.py, tests/test_bench.py).
   ncclBroadcast of x, ncclAllGather of the padded y, unpadded by
   hspmv_get_y; a C4-shaped banded CSR matrix and a CSR-3 matrix whose
   splits fall (unevenly) on super-super-row boundaries;
-* bench.py --gpus 2 under torch.distributed.run with the "nccl" (RCCL)
-  backend, one process per GPU: the driver's N > 1 command, whose y check
-  must pass.
+* plain ``bench.py --gpus 2`` (it starts torch.distributed.run itself) with
+  the "nccl" (RCCL) backend, one process per GPU: the driver's N > 1
+  command, whose y check must pass.
 y is checked against the oracle bit for bit (every row here has <= 40
 nonzeros: the ordered sums)."""
 import json
 import os
-import socket
 import subprocess
 import sys
 from pathlib import Path
@@ -86,14 +85,10 @@ def test_library_partition_distinct_devices_csr3_uneven_ssr_splits():
 
 def test_bench_nccl_two_ranks():
     need(2)
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    env = dict(os.environ, PYTHONUNBUFFERED="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-                          "--master-port", str(port), str(REPO / "bench.py"), "--gpus", "2",
+    # exactly the driver's command: no launcher, no extra environment
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONUNBUFFERED"] = "1"
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2",
                           "--steps", "20", "--warmup", "3", "--cold-steps", "2"],
                          cwd=REPO, env=env, capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, out.stderr[-3000:]

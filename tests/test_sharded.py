@@ -7,7 +7,7 @@ unpadded by hspmv_get_y.  On a one-GPU box this runs as
   * devices [0, 0, (0)]: several shards on one device, exchanged by
     device-to-device copies (the partition, uneven SSR-aligned splits, an
     empty shard and the unpadding all run).
-Each y is checked against the oracle; rows of <= 32 nonzeros bitwise."""
+Each y is checked against the oracle; rows of <= 40 nonzeros bitwise."""
 import numpy as np
 import pytest
 
@@ -28,7 +28,7 @@ def check(A, x, y):
     y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
     absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
     assert fp64_tol_ok(y, y64, absrow)
-    short = np.diff(A.row_ptr) <= 32
+    short = np.diff(A.row_ptr) <= 40
     assert np.array_equal(y[short], y64[short])
 
 
@@ -81,7 +81,7 @@ def test_sharded_csort_and_fp32():
     with hspmv.SpMV(A, devices=[0, 0, 0], kernel="stream") as op:
         y = op(x)
     y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
-    short = np.diff(A.row_ptr) <= 32
+    short = np.diff(A.row_ptr) <= 40
     assert np.array_equal(y[short].view(np.uint32), y32[short].view(np.uint32))
 
 
