@@ -174,10 +174,11 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   S *acc = reinterpret_cast<S *>(smem);
   constexpr int NW = kCsortThreads / kWave;
   const int b = blockIdx.x;
-  if (trace && threadIdx.x == 0) {  // diagnostic builds only (DevCsort.trace)
-    trace[3 * b] = __builtin_amdgcn_s_memrealtime();
-    trace[3 * b + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 20) |
-                       ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32);
+  unsigned long long *tr = trace ? trace + (int64_t)b * kCsortTraceSlots : nullptr;
+  if (tr && threadIdx.x == 0) {  // diagnostic builds only (DevCsort.trace)
+    tr[0] = __builtin_amdgcn_s_memrealtime();
+    tr[2] = __builtin_amdgcn_s_getreg((31 << 11) | 20) |
+            ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32);
   }
   const int h = b % H;  // the column part; its rows: the part's own row block
   const int32_t c0 = blk_c[b], c1 = blk_c[b + 1];
@@ -186,6 +187,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   const int32_t nr = r1 - r0, nv = v1 - v0;
   for (int32_t i = threadIdx.x; i <= nr + nv; i += kCsortThreads) acc[i] = S(0);  // + dummy
   __syncthreads();
+  if (tr && threadIdx.x == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
   uint32_t ix[U];
   T vv[U];
@@ -276,8 +278,12 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
 #if HSPMV_CSORT_ABL == 2 || HSPMV_CSORT_ABL == 3
   if (sink != S(0)) atomicAdd(&acc[nr + nv], sink);  // the dummy slot: keeps the products live
 #endif
+  if (tr && lane == 0) {  // this wave's end and chunk count (its LDS adds issued)
+    tr[4 + wid] = __builtin_amdgcn_s_memrealtime();
+    tr[4 + NW + wid] = (unsigned long long)(c1 > c0 + wid ? (c1 - c0 - wid + NW - 1) / NW : 0);
+  }
   __syncthreads();
-  if (trace && threadIdx.x == 0) trace[3 * b + 1] = __builtin_amdgcn_s_memrealtime();
+  if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
   if (direct) {  // one column part, no long rows: y straight from the slots
     for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) y[r0 + i] = (T)acc[i];
     return;

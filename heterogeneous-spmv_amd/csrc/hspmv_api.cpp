@@ -447,7 +447,7 @@ int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
 
 #ifdef HSPMV_ENV_KNOBS
 // Diagnostic builds only (not in hspmv.h): the last csort launch's
-// per-workgroup {start, end, XCC_ID | HW_ID << 32} (s_memrealtime ticks),
+// per-workgroup trace (kCsortTraceSlots u64 each, hspmv_internal.h),
 // when the handle was created with HSPMV_CSORT_TRACE=1.  Returns the
 // workgroup count (0: no trace).
 int hspmv_diag_csort_trace(hspmv_handle *h, unsigned long long *out, int max_wg) {
@@ -456,7 +456,7 @@ int hspmv_diag_csort_trace(hspmv_handle *h, unsigned long long *out, int max_wg)
   if (s.plan.kernel != kCsort || !s.dp.cs.trace) return 0;
   const int n = std::min(max_wg, s.dp.cs.n_wg);
   if (hipSetDevice(s.device) != hipSuccess || hipStreamSynchronize(s.stream) != hipSuccess ||
-      hipMemcpy(out, s.dp.cs.trace, 24 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+      hipMemcpy(out, s.dp.cs.trace, 8 * kCsortTraceSlots * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
     return 0;
   return n;
 }

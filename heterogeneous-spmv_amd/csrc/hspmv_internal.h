@@ -57,6 +57,7 @@ struct Tuning {
   int stream_waves = 0;     // 0 auto, 1/2/4
   int deterministic = 0;    // 1: only kernels whose y bits never depend on scheduling
   int placement_trials = 0; // 0/1 off, K <= 8 array sets
+  int ssr_align = -1;       // SSR plan: waves take 64-row aligned pieces of their SSR (-1: default)
   // A/B only (diagnostic builds)
   int contig = 0;           // hipDeviceMallocContiguous allocations
   int xd_waves = 0;         // packed CSR3 tasks per dictionary block (0: 4; 8)
@@ -95,6 +96,11 @@ constexpr int32_t kLongChunk = 4096;
 // blk_v[b+1]).  Built by build_csort (hspmv_csort_build.cpp).
 constexpr int kCsortThreads = 1024;
 constexpr int kCsortMaxLds = 160 * 1024;
+// Diagnostic trace of a csort launch (DevCsort.trace, HSPMV_CSORT_TRACE=1):
+// per workgroup kCsortTraceSlots u64 = {start, end, XCC_ID | HW_ID << 32,
+// after the slot-zeroing barrier, then per wave: its end (after its last
+// chunk), then per wave: the chunks it ran} (s_memrealtime, 100 MHz).
+constexpr int kCsortTraceSlots = 4 + 2 * (kCsortThreads / 64);
 struct DevCsort {
   int32_t n_wg = 0, H = 1, u = 16, direct = 0, n_long = 0;
   bool nontemporal = true;
@@ -123,6 +129,10 @@ struct DevPlan {
   // boundaries (HSPMV_CSR3_PLAN=ssr).
   const int32_t *task_start = nullptr;
   int32_t n_tasks = 0;
+  // 1: a task's 64-row groups end on multiples of 64 (its first group may be
+  // shorter) -- the SSR plan's aligned cut (ssr_tasks_aligned); 0: groups of
+  // 64 rows from the task's first row
+  int32_t task_align = 0;
   // split rows
   int32_t long_t = 0x7fffffff;  // rows with more nonzeros are split rows
   int32_t n_long = 0, n_chunks = 0;

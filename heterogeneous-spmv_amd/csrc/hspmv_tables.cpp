@@ -235,6 +235,45 @@ void ssr_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> &o,
   ts[(size_t)(nssr * W)] = (int32_t)m;
 }
 
+// The SSR plan's aligned cut (Tuning.ssr_align): the same one workgroup of W
+// waves per super-super-row, but the waves take the SSR's 64-row ALIGNED
+// pieces -- [R0, next multiple of 64), whole aligned groups, [last multiple,
+// R1) -- instead of nonzero-balanced runs of whole super-rows, so a wave's
+// y stores cover whole cache lines except at the SSR's two edges (the
+// kernel's groups end on multiples of 64: DevPlan.task_align).  With more
+// pieces than waves, the adjacent pair with the fewest nonzeros merges until
+// W remain; with fewer, the last waves get empty tasks.
+bool ssr_aligned(const Tuning &t) { return t.csr3_plan == HSPMV_CSR3_PLAN_SSR && t.ssr_align > 0; }
+
+void ssr_tasks_aligned(const int32_t *rp, int64_t m, const std::vector<int32_t> &o,
+                       const std::vector<int32_t> &in, int W, std::vector<int32_t> &ts) {
+  const int64_t nssr = (int64_t)o.size() - 1;
+  ts.assign((size_t)(nssr * W + 1), 0);
+  std::vector<int32_t> cut;
+  for (int64_t b = 0; b < nssr; ++b) {
+    const int32_t R0 = in[(size_t)o[(size_t)b]], R1 = in[(size_t)o[(size_t)b + 1]];
+    cut.clear();
+    cut.push_back(R0);
+    for (int32_t a = (R0 & ~63) + 64; a < R1; a += 64) cut.push_back(a);
+    cut.push_back(R1);
+    while ((int)cut.size() - 1 > W) {  // merge the lightest adjacent pair
+      size_t best = 1;
+      int64_t bn = INT64_MAX;
+      for (size_t i = 1; i + 1 < cut.size(); ++i) {
+        const int64_t nz = (int64_t)rp[cut[i + 1]] - rp[cut[i - 1]];
+        if (nz < bn) {
+          bn = nz;
+          best = i;
+        }
+      }
+      cut.erase(cut.begin() + (ptrdiff_t)best);
+    }
+    for (int w = 0; w < W; ++w)
+      ts[(size_t)(b * W + w)] = w + 1 < (int)cut.size() ? cut[(size_t)w] : R1;
+  }
+  ts[(size_t)(nssr * W)] = (int32_t)m;
+}
+
 // Task cut of the packed CSR-3 plan: 64-row groups aligned to multiples of 64
 // rows (default), or whole super-rows packed up to 64 rows
 // (Tuning.csr3_plan = HSPMV_CSR3_PLAN_PACKED, pack_csr3_tasks).  The row sums are row-local, so y is
@@ -318,7 +357,10 @@ void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner
   if (!csr3_packed(tune)) {
     if (!inner || !outer || outer->size() < 2) return;
     *waves = ssr_waves((double)m / (double)(outer->size() - 1));
-    ssr_tasks(rp, m, *outer, *inner, *waves, ts);
+    if (ssr_aligned(tune))
+      ssr_tasks_aligned(rp, m, *outer, *inner, *waves, ts);
+    else
+      ssr_tasks(rp, m, *outer, *inner, *waves, ts);
     return;
   }
   const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
@@ -722,6 +764,7 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
     HIP_TRY(hipMemcpy(s.d_task, s.h_tasks.data(), 4 * s.h_tasks.size(), hipMemcpyHostToDevice));
     s.dp.task_start = s.d_task;
     s.dp.n_tasks = (int32_t)(s.h_tasks.size() - 1);
+    s.dp.task_align = ssr_aligned(s.tune) ? 1 : 0;
   }
   return HSPMV_OK;
 }
