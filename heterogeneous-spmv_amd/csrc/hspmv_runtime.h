@@ -97,6 +97,7 @@ struct Shard {
   // placement trials (place_shard): SpMV time of each array set, the kept one
   std::vector<double> place_us;
   int place_pick = 0;
+  double trial_us[2] = {0, 0};  // kernel_trial: CSR3, STREAM mean SpMV (us); 0 = no trial
   Tuning tune;  // the handle's planner choices (hspmv_options)
 };
 
@@ -151,6 +152,7 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
                  int64_t ssr0, int64_t ssr1, int64_t y_rows_alloc, unsigned flags);
 int finish_shard(Shard &s, int dtype, unsigned flags, void *stream);
 int place_shard(Shard &s, int64_t n, int dtype);
+int kernel_trial(Shard &s, int64_t n, int dtype, unsigned flags);
 
 // ---- hspmv_tables.cpp
 int64_t count_distinct_cols(const int32_t *col, int64_t nnz, int64_t n);

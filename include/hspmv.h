@@ -178,6 +178,12 @@ typedef struct {
   int64_t csort_chunks;     /* CSORT: 64*U-entry chunks of the launch       */
   int64_t csort_seg_chunks; /* CSORT: of those, chunks stored slot-sorted
                                (crowded rows summed by a segmented scan)   */
+  /* since 1.0 */
+  int32_t kernel_trial;     /* 1: the row kernel was picked by timing both
+                               candidates at creation (a deterministic
+                               x-slab handle: CSR3 tasks vs STREAM groups)  */
+  int32_t kernel_trial_pick; /* the HSPMV_KERNEL_* kept                    */
+  double kernel_trial_us[2];  /* mean SpMV time of CSR3, STREAM (us)       */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;

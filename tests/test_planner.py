@@ -109,3 +109,33 @@ def test_rcm_mesh_stencil_small_and_csr2():
         y3, i3 = run(A, x, maps)
         assert i3["kernel_name"] == "csr3"
         assert np.array_equal(y3, y)
+
+
+@pytest.mark.parametrize("cfg", ["c5", "c5r"])
+def test_deterministic_slab_handle_times_both_row_kernels(cfg):
+    """A deterministic handle over irregular gathers (csort off, x slabs on)
+    times the CSR3 tasks and the STREAM groups on its own arrays at creation
+    and keeps the faster (hspmv_shard.cpp kernel_trial): C5's random rows
+    and c5r's RCM-ordered rows preferred opposite kernels in r04.  y is the
+    ordered row sum either way: bitwise against the forced kernels' y."""
+    from hspmv import dist as hdist
+    sh = hdist.build_shard(cfg, 0, 1)
+    A, maps = sh.A, sh.maps
+    x = gen.rand_x(A.n, 11).astype(A.val.dtype)
+    y, info = run(A, x, maps, options={"deterministic": 1})
+    assert info["deterministic"] == 1
+    if cfg == "c5":
+        assert info["x_slabs"] > 0  # random columns over an 8 MB x
+    # the trial runs exactly when the handle streams x slabs
+    assert info["kernel_trial"] == (1 if info["x_slabs"] > 0 else 0)
+    if info["kernel_trial"]:
+        t3, ts = info["kernel_trial_us"]
+        assert info["kernel_name"] == ("stream" if ts < t3 else "csr3")
+        assert info["kernel_trial_pick"] == info["kernel"]
+    for kernel in ("csr3", "stream"):
+        yk, ik = run(A, x, maps, kernel=kernel, options={"deterministic": 1})
+        assert ik["kernel_name"] == kernel and ik["kernel_trial"] == 0
+        assert np.array_equal(yk.view(np.uint32), y.view(np.uint32))
+    y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    short = np.diff(A.row_ptr) <= SERIAL_MAX
+    assert np.array_equal(y[short].view(np.uint32), y32[short].view(np.uint32))
