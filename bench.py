@@ -277,9 +277,9 @@ def cpu_c1(budget_s: float) -> dict:
             "cgroup_cpu_quota": first["cgroup_cpu_quota"], "x": legs,
             "value": legs["rand:42"]["static"]["gflops"], "unit": "GFLOP/s",
             "sample": (f"gen.laplace2d(1000, 1000): m={A.m}, nnz={A.nnz}, fp64 CSR; omp_spmv restatement "
-                       f"(oracle/spmv_oracle.c), {first['cores']} threads, 5 warm-ups + "
-                       f"{first['guided']['runs']} timed runs per (x, schedule); value = x rand:42, "
-                       f"static, 2 nnz / TimeMin")}
+                       f"(oracle/spmv_oracle.c), {first['cores']} threads, 5 warm-ups + the timed runs "
+                       f"in x[x][schedule].runs (a {max(0.2, budget_s):.1f} s budget per x); value = "
+                       f"x rand:42, static, 2 nnz / TimeMin")}
 
 
 def single_gpu_point(args, stream, cfg: str):
