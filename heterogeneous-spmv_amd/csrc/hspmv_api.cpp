@@ -104,10 +104,6 @@ int create_single(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *
     free_shard(s, h->borrowed);
     return rc;
   }
-  if (!devptrs && (rc = kernel_trial(s, A->n, A->dtype, flags))) {
-    free_shard(s, h->borrowed);
-    return rc;
-  }
   if (!devptrs && (rc = place_shard(s, A->n, A->dtype))) {
     free_shard(s, h->borrowed);
     return rc;
@@ -433,10 +429,8 @@ static int fill_info(hspmv_handle *h, hspmv_info *out) {
   out->csort_slot_bytes = s.plan.kernel == kCsort ? (s.dp.cs.slot32 ? 4 : 8) : 0;
   out->csort_row_blocks = s.plan.kernel == kCsort ? s.dp.cs.row_blocks : 0;
   out->rccl_version = h->rccl_version;
-  out->kernel_trial = s.trial_us[0] > 0 ? 1 : 0;
-  out->kernel_trial_pick = out->kernel_trial ? s.plan.kernel : 0;
-  out->kernel_trial_us[0] = s.trial_us[0];
-  out->kernel_trial_us[1] = s.trial_us[1];
+  out->slab_kernel_rule = s.heavy_frac < 0 ? 0 : (s.A.slab_stream ? 2 : 1);
+  out->heavy_group_frac = s.heavy_frac < 0 ? 0.0 : s.heavy_frac;
   for (auto &sh : h->shards)
     if (sh.plan.kernel == kCsort) {
       out->csort_chunks += sh.csort_chunks;

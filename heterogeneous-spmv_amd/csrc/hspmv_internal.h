@@ -35,6 +35,7 @@ struct DevCSR {
   int32_t task_waves = 4;     // CSR3 wave tasks per workgroup: 4 (8 with 8-task dictionary
                               // blocks); the SSR plan: ssr_waves() per super-super-row
   bool has_csort = false;     // column-sorted row blocks were built (irregular gathers)
+  bool slab_stream = false;   // x-slab passes with CSR-3 tasks: AUTO runs STREAM (slab_kernel_rule)
 };
 
 // Planner choices of one handle.  The first block mirrors hspmv_options

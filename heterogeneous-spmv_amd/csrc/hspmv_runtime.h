@@ -97,7 +97,7 @@ struct Shard {
   // placement trials (place_shard): SpMV time of each array set, the kept one
   std::vector<double> place_us;
   int place_pick = 0;
-  double trial_us[2] = {0, 0};  // kernel_trial: CSR3, STREAM mean SpMV (us); 0 = no trial
+  double heavy_frac = -1.0;  // x-slab handles with CSR3 tasks: nonzeros in heavy 64-row groups (slab_kernel_rule)
   Tuning tune;  // the handle's planner choices (hspmv_options)
 };
 
@@ -152,7 +152,6 @@ int upload_shard(Shard &s, const hspmv_csr *A, const hspmv_csr3_maps *mp, int64_
                  int64_t ssr0, int64_t ssr1, int64_t y_rows_alloc, unsigned flags);
 int finish_shard(Shard &s, int dtype, unsigned flags, void *stream);
 int place_shard(Shard &s, int64_t n, int dtype);
-int kernel_trial(Shard &s, int64_t n, int dtype, unsigned flags);
 
 // ---- hspmv_tables.cpp
 int64_t count_distinct_cols(const int32_t *col, int64_t nnz, int64_t n);

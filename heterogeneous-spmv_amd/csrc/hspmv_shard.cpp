@@ -173,36 +173,6 @@ static double time_shard(Shard &s, int dtype) {
   return best;
 }
 
-// Kernel trial.  A deterministic handle (hspmv_options.deterministic: the
-// column-sorted kernel is off) over irregular gathers runs its row kernel
-// in x-slab passes, and whether the CSR3 tasks or the STREAM groups stream
-// those passes faster depends on the row order, not on anything the planner
-// sees cheaply: C5 (random columns) STREAM 263 vs CSR3 313 us, c5r (the same
-// matrix RCM-ordered) CSR3 307 vs STREAM 435 (DESIGN.md §10, r04 zoo).  The
-// two kernels share every table of such a handle (slab copies, split rows;
-// the CSR3 task table is simply unused by STREAM), so both are timed on the
-// handle's own arrays (time_shard) and the faster launch plan is kept.  y is
-// bitwise the same either way (row-local ordered sums).  Single-GPU handles
-// with owned arrays under the AUTO kernel.
-int kernel_trial(Shard &s, int64_t n, int dtype, unsigned flags) {
-  if (!s.tune.deterministic || s.n_slabs <= 0 || s.plan.kernel != kCsr3 || (flags & 0xFu) != kAuto ||
-      s.A.m == 0 || !s.d_x || !s.d_y)
-    return HSPMV_OK;
-  const LaunchPlan alt = plan_launch(s.A, dtype, (flags & ~0xFu) | kStream, s.mean_rows_per_ssr, 0, s.tune);
-  if (alt.kernel != kStream) return HSPMV_OK;
-  HIP_TRY(hipSetDevice(s.device));
-  HIP_TRY(hipMemsetAsync(s.d_x, 0, dtype_size(dtype) * (size_t)n, s.stream));
-  const double t3 = time_shard(s, dtype);
-  const LaunchPlan keep = s.plan;
-  s.plan = alt;
-  const double ts = time_shard(s, dtype);
-  if (t3 < 0 || ts < 0) return set_error(HSPMV_E_HIP, "kernel trial: launch failed");
-  s.trial_us[0] = t3;
-  s.trial_us[1] = ts;
-  if (ts >= t3) s.plan = keep;
-  return HSPMV_OK;
-}
-
 // Placement trials.  Where a handle's streamed arrays land in HBM moves the
 // HBM-bound row kernels by up to ~10 %: identical C3 handles created one
 // after another in one process ran 101.0, 105.4 and 110.8 us, each stable

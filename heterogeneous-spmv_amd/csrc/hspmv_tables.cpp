@@ -591,6 +591,36 @@ int build_xslabs(Shard &s, const int32_t *rp, const int32_t *col, const void *va
   return HSPMV_OK;
 }
 
+// Which row kernel streams the x-slab passes of a handle that has CSR-3
+// tasks (irregular gathers from a wide x with the column-sorted kernel off:
+// deterministic handles, csort = -1).  The CSR3 tasks are capped at 2048
+// nonzeros, so they balance 64-row groups a power-law ordering makes heavy;
+// where the groups are balanced anyway the task table only costs.  r04 zoo
+// (DESIGN.md §10): C5's random row order -- 6.5 % of the nonzeros in heavy
+// groups -- STREAM 263 vs CSR3 313 us; c5r, the same rows RCM-ordered --
+// 19.2 % heavy, the largest group 61.6 K nonzeros -- CSR3 307 vs STREAM 435.
+// The cut at 1/8 of the nonzeros separates the two.  A rule, not a timing
+// trial: a deterministic handle's y must not depend on which kernel won a
+// race at creation (the two kernels sum rows above kSerialMax nonzeros in
+// different orders).
+constexpr double kSlabHeavyShare = 0.125;
+
+void slab_kernel_rule(Shard &s, const int32_t *rp, int64_t m, unsigned flags) {
+  const int32_t long_t = (flags & HSPMV_FLAG_NO_SPLIT) ? INT32_MAX : kLongRow;
+  int64_t heavy = 0, total = 0;
+  for (int64_t g = 0; g < m; g += 64) {
+    int64_t in = 0;
+    for (int64_t r = g; r < std::min(m, g + 64); ++r) {
+      const int64_t len = rp[r + 1] - rp[r];
+      in += len > long_t ? 0 : len;
+    }
+    total += in;
+    heavy += in > task_nnz_budget(s.tune) ? in : 0;
+  }
+  s.heavy_frac = total ? (double)heavy / (double)total : 0.0;
+  s.A.slab_stream = s.heavy_frac < kSlabHeavyShare;
+}
+
 // Host-side tables that need the columns (built at upload, while they are
 // at hand): the CSR-3 packed tasks, the block x dictionaries, and (without
 // dictionaries) the 16-bit column offsets and the x windows of both row
@@ -633,6 +663,7 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
   if (s.n_slabs) {  // slab passes read 32-bit columns from global x
     s.A.col_span_bits = 31;
     s.A.n_slabs = s.n_slabs;
+    if (!s.h_tasks.empty()) slab_kernel_rule(s, rp, m, flags);
     return HSPMV_OK;
   }
   s.h_xwin = xwin_table(rp, col, m, nullptr, s.tune);

@@ -271,7 +271,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   // groups exceed the task budget, hspmv_tables.cpp build_tasks)
   const bool tasks = A.n_ssr > 0 || packed_tasks > 0;
   if (k == kAuto)
-    p.kernel = A.has_csort ? kCsort : (tasks ? kCsr3 : kStream);
+    p.kernel = A.has_csort ? kCsort : (tasks && !A.slab_stream ? kCsr3 : kStream);
   else
     p.kernel = (int)k;
   if (p.kernel == kCsort && !A.has_csort) p.kernel = tasks ? kCsr3 : kStream;

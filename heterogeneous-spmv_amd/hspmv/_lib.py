@@ -119,8 +119,8 @@ class Info(C.Structure):
                 ("csort_slot_bytes", C.c_int32), ("csort_row_blocks", C.c_int32),
                 ("rccl_version", C.c_int32), ("reserved0", C.c_int32),
                 ("csort_chunks", C.c_int64), ("csort_seg_chunks", C.c_int64),
-                ("kernel_trial", C.c_int32), ("kernel_trial_pick", C.c_int32),
-                ("kernel_trial_us", C.c_double * 2)]
+                ("slab_kernel_rule", C.c_int32), ("reserved1", C.c_int32),
+                ("heavy_group_frac", C.c_double)]
 
 
 CSR3_PLANS = {"auto": 0, "aligned": 1, "packed": 2, "ssr": 3}

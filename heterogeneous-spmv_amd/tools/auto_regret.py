@@ -13,7 +13,11 @@ matrix reports AUTO's kernel and time, the fastest variant and
 regret = t_auto / t_best.
 
     python heterogeneous-spmv_amd/tools/auto_regret.py [--zoo all|name,...]
-           [--rounds 3] [--iters 20] [--out profiles/rNN_auto_regret.jsonl]
+           [--rounds 3] [--iters 20] [--deterministic] [--out profiles/rNN_auto_regret.jsonl]
+
+--deterministic: every handle with hspmv_options.deterministic = 1 (the
+column-sorted kernel is refused and dropped from the variants), the
+planner a reproducible-results caller gets.
 """
 from __future__ import annotations
 
@@ -98,7 +102,7 @@ def build(name: str):
     raise ValueError(name)
 
 
-def variants(A, maps):
+def variants(A, maps, deterministic=False):
     d = A.nnz / max(A.m, 1)
     v = [("auto", dict(kernel="auto"), maps)]
     if maps is not None:
@@ -107,6 +111,8 @@ def variants(A, maps):
     for L in ((4, 8) if d < 16 else (16, 64)):
         v.append((f"vector{L}", dict(kernel="vector", lanes=L), None))
     v.append(("csr3", dict(kernel="csr3"), maps))
+    if deterministic:
+        return [(n, dict(kw, options={"deterministic": 1}), mp) for n, kw, mp in v]
     v.append(("csort", dict(kernel="csort"), None))
     return v
 
@@ -116,6 +122,7 @@ def main():
     ap.add_argument("--zoo", default="all")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--deterministic", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     import oracle
@@ -136,7 +143,7 @@ def main():
               file=sys.stderr, flush=True)
         dev = sweep.DeviceMatrix(A, x)
         ops = []
-        for vname, kw, mp in variants(A, maps):
+        for vname, kw, mp in variants(A, maps, a.deterministic):
             try:
                 op = dev.spmv(mp, **kw)
             except hspmv.HspmvError as e:  # e.g. csort refused for this shape
@@ -165,6 +172,7 @@ def main():
         best = min(timed, key=lambda k: timed[k]["t_us"]) if timed else None
         auto = res.get("auto")
         rec = {"matrix": name, "desc": desc, "m": A.m, "n": A.n, "nnz": A.nnz,
+               "deterministic": a.deterministic,
                "dtype": str(A.val.dtype), "maps": maps is not None,
                "auto_kernel": auto["kernel"] if auto else None,
                "auto_us": auto["t_us"] if auto else None,

@@ -179,11 +179,14 @@ typedef struct {
   int64_t csort_seg_chunks; /* CSORT: of those, chunks stored slot-sorted
                                (crowded rows summed by a segmented scan)   */
   /* since 1.0 */
-  int32_t kernel_trial;     /* 1: the row kernel was picked by timing both
-                               candidates at creation (a deterministic
-                               x-slab handle: CSR3 tasks vs STREAM groups)  */
-  int32_t kernel_trial_pick; /* the HSPMV_KERNEL_* kept                    */
-  double kernel_trial_us[2];  /* mean SpMV time of CSR3, STREAM (us)       */
+  int32_t slab_kernel_rule; /* x-slab handles that have CSR-3 tasks (the
+                               AUTO kernel): 1 = CSR3 tasks, since heavy
+                               64-row groups (> 2048 nonzeros) hold >= 1/8
+                               of the nonzeros; 2 = STREAM groups (balanced
+                               groups); 0 = the rule did not apply          */
+  int32_t reserved1;
+  double heavy_group_frac;  /* the share of nonzeros in heavy 64-row groups
+                               the rule read (0 when it did not apply)     */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;

@@ -112,30 +112,35 @@ def test_rcm_mesh_stencil_small_and_csr2():
 
 
 @pytest.mark.parametrize("cfg", ["c5", "c5r"])
-def test_deterministic_slab_handle_times_both_row_kernels(cfg):
+def test_slab_handles_pick_the_row_kernel_by_group_balance(cfg):
     """A deterministic handle over irregular gathers (csort off, x slabs on)
-    times the CSR3 tasks and the STREAM groups on its own arrays at creation
-    and keeps the faster (hspmv_shard.cpp kernel_trial): C5's random rows
-    and c5r's RCM-ordered rows preferred opposite kernels in r04.  y is the
-    ordered row sum either way: bitwise against the forced kernels' y."""
+    with CSR-3 tasks runs STREAM when its 64-row groups are balanced and the
+    CSR3 tasks when heavy groups (> 2048 nonzeros) hold >= 1/8 of the
+    nonzeros (hspmv_tables.cpp slab_kernel_rule): C5's random rows (6.5 %)
+    and c5r's RCM-ordered rows (19.2 %) go opposite ways, as their r04
+    timings did.  A rule, so two deterministic handles always agree bit for
+    bit; y bitwise against the forced kernel of the same choice, and on rows
+    of <= 40 nonzeros against the other kernel and the reference loop."""
     from hspmv import dist as hdist
     sh = hdist.build_shard(cfg, 0, 1)
     A, maps = sh.A, sh.maps
     x = gen.rand_x(A.n, 11).astype(A.val.dtype)
     y, info = run(A, x, maps, options={"deterministic": 1})
-    assert info["deterministic"] == 1
-    if cfg == "c5":
-        assert info["x_slabs"] > 0  # random columns over an 8 MB x
-    # the trial runs exactly when the handle streams x slabs
-    assert info["kernel_trial"] == (1 if info["x_slabs"] > 0 else 0)
-    if info["kernel_trial"]:
-        t3, ts = info["kernel_trial_us"]
-        assert info["kernel_name"] == ("stream" if ts < t3 else "csr3")
-        assert info["kernel_trial_pick"] == info["kernel"]
+    assert info["deterministic"] == 1 and info["x_slabs"] > 0
+    want = {"c5": ("stream", 2), "c5r": ("csr3", 1)}[cfg]
+    assert (info["kernel_name"], info["slab_kernel_rule"]) == want
+    lens = np.diff(A.row_ptr)
+    lens_in = np.where(lens > 4096, 0, lens).astype(np.int64)
+    g = np.add.reduceat(lens_in, np.arange(0, A.m, 64))
+    assert abs(info["heavy_group_frac"] - g[g > 2048].sum() / g.sum()) < 1e-9
+    y2, _ = run(A, x, maps, options={"deterministic": 1})
+    assert np.array_equal(y2.view(np.uint32), y.view(np.uint32))
+    short = lens <= SERIAL_MAX
     for kernel in ("csr3", "stream"):
         yk, ik = run(A, x, maps, kernel=kernel, options={"deterministic": 1})
-        assert ik["kernel_name"] == kernel and ik["kernel_trial"] == 0
-        assert np.array_equal(yk.view(np.uint32), y.view(np.uint32))
+        assert ik["kernel_name"] == kernel
+        if kernel == want[0]:
+            assert np.array_equal(yk.view(np.uint32), y.view(np.uint32))
+        assert np.array_equal(yk[short].view(np.uint32), y[short].view(np.uint32))
     y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
-    short = np.diff(A.row_ptr) <= SERIAL_MAX
     assert np.array_equal(y[short].view(np.uint32), y32[short].view(np.uint32))
