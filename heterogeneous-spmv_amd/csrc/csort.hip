@@ -169,8 +169,9 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     const int32_t *__restrict__ vslice, const int32_t *__restrict__ cbase,
     const void *__restrict__ ent, const T *__restrict__ val, const T *__restrict__ x,
     S *__restrict__ part, S *__restrict__ spart, T *__restrict__ y,
-    unsigned long long *__restrict__ trace) {
+    unsigned long long *__restrict__ trace, int32_t dyn) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int32_t next_chunk;  // dyn: the workgroup's chunk queue head
   S *acc = reinterpret_cast<S *>(smem);
   constexpr int NW = kCsortThreads / kWave;
   const int b = blockIdx.x;
@@ -186,6 +187,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   const int32_t v0 = blk_v[b], v1 = blk_v[b + 1];
   const int32_t nr = r1 - r0, nv = v1 - v0;
   for (int32_t i = threadIdx.x; i <= nr + nv; i += kCsortThreads) acc[i] = S(0);  // + dummy
+  if (threadIdx.x == 0) next_chunk = c0 + NW;
   __syncthreads();
   if (tr && threadIdx.x == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
@@ -198,7 +200,21 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   // in flight (software pipelining across the wave's chunks)
   if constexpr (PF)
     if (c0 + wid < c1) load_entries<T, U, NT, WIDE>(ent, val, c0 + wid, lane, ix, vv);
-  for (int32_t c = c0 + wid; c < c1; c += NW) {  // wave-uniform
+  // Chunk order.  dyn: wave w starts at chunk c0 + w and then takes the
+  // next unclaimed chunk of the workgroup (one LDS atomic per chunk, claimed
+  // a chunk ahead so PF can load it).  Without it wave w takes every NW-th
+  // chunk -- and the 16 waves finish in four tiers of four (one wave per
+  // SIMD each, oldest first: C5 ~39 / 57 / 77 / 94 us), the last quarter of
+  // the workgroup's time run by 4 waves (profiles/r05b/csort_trace.jsonl).
+  int32_t cn_done = 0;
+  for (int32_t c = c0 + wid; c < c1;) {  // wave-uniform
+    int32_t cn = c + NW;
+    if (dyn) {
+      int32_t got = 0;
+      if (lane == 0) got = atomicAdd(&next_chunk, 1);
+      cn = __builtin_amdgcn_readfirstlane(got);
+    }
+    ++cn_done;
     // bit 31 of the chunk base: a "segmented" chunk (see below)
     const uint32_t cb = (uint32_t)wave_uniform(cbase[wave_uniform(c)]);
     const int32_t base = (int32_t)(cb & 0x7fffffffu);
@@ -220,7 +236,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     }
     if constexpr (PF) {
       __builtin_amdgcn_sched_barrier(0);
-      if (c + NW < c1) load_entries<T, U, NT, WIDE>(ent, val, c + NW, lane, ix, vv);
+      if (cn < c1) load_entries<T, U, NT, WIDE>(ent, val, cn, lane, ix, vv);
       __builtin_amdgcn_sched_barrier(0);
     }
     if (!seg) {
@@ -274,13 +290,14 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
         if (lane == kWave - 1 || ((msk >> (lane + 1)) & 1ull)) atomicAdd(&acc[sl], v);
       }
     }
+    c = cn;
   }
 #if HSPMV_CSORT_ABL == 2 || HSPMV_CSORT_ABL == 3
   if (sink != S(0)) atomicAdd(&acc[nr + nv], sink);  // the dummy slot: keeps the products live
 #endif
   if (tr && lane == 0) {  // this wave's end and chunk count (its LDS adds issued)
     tr[4 + wid] = __builtin_amdgcn_s_memrealtime();
-    tr[4 + NW + wid] = (unsigned long long)(c1 > c0 + wid ? (c1 - c0 - wid + NW - 1) / NW : 0);
+    tr[4 + NW + wid] = (unsigned long long)cn_done;
   }
   __syncthreads();
   if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
@@ -361,7 +378,7 @@ void launch_csort_main(const DevCsort &c, const T *x, S *part, S *spart, T *y, h
   hipLaunchKernelGGL((hspmv_csort<T, S, U, NT, PF, WIDE>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
                      (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
                      c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y,
-                     c.trace);
+                     c.trace, c.dyn ? 1 : 0);
 }
 
 template <typename T, typename S, int U, bool NT>

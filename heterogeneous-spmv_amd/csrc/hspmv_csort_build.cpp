@@ -61,7 +61,9 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, s.device) != hipSuccess ||
       lds_max <= 0)
     return HSPMV_OK;
-  lds_max = std::min(lds_max, kCsortMaxLds);
+  // the kernel's static LDS (its chunk-queue head, 16 B with alignment)
+  // comes out of the same budget
+  lds_max = std::min(lds_max, kCsortMaxLds) - 16;
   const Tuning &tn = s.tune;
   if (tn.csort_lds_cap > 0) lds_max = std::min(lds_max, tn.csort_lds_cap);  // A/B
   const bool slot32 = dtype == HSPMV_F32 && tn.csort_slot32 == 1;
@@ -538,6 +540,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.slot32 = slot32;
   c.wide = wide;
   c.fin_rows = tn.csort_fin_rows;
+  c.dyn = tn.csort_dyn > 0;  // A/B first (r05)
   c.m = m;
   c.lds_bytes = (int32_t)(slot_bytes * max_slots_used);
   c.blk_c = s.d_cs_blk_c;

@@ -75,6 +75,7 @@ struct Tuning {
   int csort_long = 0;                    // rows above this many nonzeros are sliced (0: kLongRow)
   int csort_balance = 0;                 // -1: equal-width column parts, nnz-balanced rows (r03)
   int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4)
+  int csort_dyn = -1;                    // chunks claimed from an LDS queue (-1: the library's choice)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
 };
@@ -108,6 +109,7 @@ struct DevCsort {
   bool prefetch = false;  // next chunk's entries loaded during this chunk's gathers
   bool slot32 = false;    // fp32 LDS row slots and partials (fp32 data; A/B)
   bool wide = false;      // 16-byte entry loads (host-interleaved layout)
+  bool dyn = false;       // waves claim the workgroup's chunks from an LDS queue
   int32_t fin_rows = 0;   // rows per finishing-pass thread (0: 4, or the most m allows)
   int64_t m = 0;
   int32_t lds_bytes = 0;
