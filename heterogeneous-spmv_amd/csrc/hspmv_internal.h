@@ -76,6 +76,7 @@ struct Tuning {
   int csort_balance = 0;                 // -1: equal-width column parts, nnz-balanced rows (r03)
   int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4)
   int csort_dyn = -1;                    // chunks claimed from an LDS queue (-1: the library's choice)
+  int early_bounds = -1;                 // CSR3 + x dictionaries: bounds before the staging (-1: default)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
 };
@@ -180,6 +181,7 @@ struct LaunchPlan {
   int32_t xcd_chunk = 1;   // blocks per XCD turn (1 = dispatch order; see xcd_chunk_remap)
   int32_t groups = 1;      // STREAM: 64-row groups per wave (next group's rp prefetched)
   int32_t carry = 0;       // STREAM/CSR3: rows start from y (x-slab passes after the first)
+  int32_t early_bounds = 0; // CSR3 + x dictionaries: task / row bounds loaded before the staging
   int64_t blocks = 0;
 };
 

@@ -606,7 +606,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
 template <typename T, bool NT, int U, bool PF, int C16, int W, bool XW, bool XD>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, int32_t y_nt, int32_t carry, int32_t align,
-    const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin, XDict xd,
+    int32_t early, const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin, XDict xd,
     const int32_t *__restrict__ rp, ColSrc cs, const T *__restrict__ val,
     const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[W * kWave * U];
@@ -623,17 +623,30 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     bt[7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
   }
 #endif
+  const int64_t t = blk * W + wid;
+  // early (XD): the task bounds and the first group's row bounds are loaded
+  // BEFORE the dictionary staging, so their round trips overlap it instead
+  // of following its barrier
+  int32_t r0 = 0, r1 = 0, beg = 0, end = 0;
+  auto task_bounds = [&]() {
+    // both task bounds in one scalar load (K$), not a vector round trip
+    const int64_t tb = sload_i64(task_start, (uint64_t)t * 4u);
+    r0 = (int32_t)tb;
+    r1 = (int32_t)(tb >> 32);
+  };
+  auto first_end = [&]() { return align ? (r0 & ~(kWave - 1)) + kWave : r0 + kWave; };
+  const bool pre = XD && early;
+  if (pre && t < n_tasks) {
+    task_bounds();
+    if (r0 < r1) group_bounds(rp, r0, min(first_end(), r1), lane, beg, end);
+  }
   // XD: the W packed tasks of the block share one staged dictionary
   if constexpr (XD) stage_xdict<T, W * 64>(reinterpret_cast<T *>(xdyn), x, xd, blk, threadIdx.x);
-  const int64_t t = blk * W + wid;
   if (t >= n_tasks) return;
 #if (HSPMV_DIAG & 8)
   const unsigned long long tb_stamp = diag_stamp();
 #endif
-  // both task bounds in one scalar load (K$), not a vector round trip
-  const int64_t tb = sload_i64(task_start, (uint64_t)t * 4u);
-  const int32_t r0 = (int32_t)tb;
-  const int32_t r1 = (int32_t)(tb >> 32);
+  if (!pre) task_bounds();
   if (r0 >= r1) return;
   T *my = lds + wid * kWave * U;
   // group-base columns: one base per packed task
@@ -655,13 +668,12 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
 #endif
   // align: groups end on multiples of 64 rows (the SSR plan's aligned
   // pieces: every y store but an SSR's first and last covers whole lines)
-  const int32_t first_end = align ? (r0 & ~(kWave - 1)) + kWave : r0 + kWave;
-  int32_t beg, end;
-  group_bounds(rp, r0, min(first_end, r1), lane, beg, end);
+  const int32_t g1_first = min(first_end(), r1);
+  if (!pre) group_bounds(rp, r0, g1_first, lane, beg, end);
 #if (HSPMV_DIAG & 8)
   HSPMV_TRACE(ts, 1, diag_stamp());
 #endif
-  for (int32_t g0 = r0, g1 = min(first_end, r1); g0 < r1; g0 = g1, g1 = min(g1 + kWave, r1)) {
+  for (int32_t g0 = r0, g1 = g1_first; g0 < r1; g0 = g1, g1 = min(g1 + kWave, r1)) {
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
     wave_rows<T, NT, U, PF, C16, XW, XD, HSPMV_COOP_GROUPS != 0>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
@@ -733,8 +745,8 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
 #define HSPMV_CSR3(W, C, XW, X)                                                               \
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C, W, XW, X>), dim3((unsigned)p.blocks),      \
                      dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,     \
-                     (int32_t)p.y_nt, p.carry, dp.task_align, dp.task_start, xw, xd, A.row_ptr, cs, \
-                     val, x, y)
+                     (int32_t)p.y_nt, p.carry, dp.task_align, p.early_bounds, dp.task_start, xw, xd,  \
+                     A.row_ptr, cs, val, x, y)
   if constexpr (XD) {  // packed tasks only (4 or 8 per block)
     if (p.waves_per_block == 8)
       HSPMV_CSR3(8, false, false, true);

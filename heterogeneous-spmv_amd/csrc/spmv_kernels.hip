@@ -382,6 +382,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   // r02r_ab_pf.jsonl)
   if (!p.prefetch && dtype == 1 && p.kernel == kCsr3 && A.has_xdict_tasks && !forced_u)
     p.prefetch = true;
+  p.early_bounds = t.early_bounds > 0 ? 1 : 0;  // A/B first (r05)
   if (t.pf >= 0) p.prefetch = t.pf != 0;  // A/B knobs (diagnostic builds only)
   if (t.y_nt >= 0) p.y_nt = t.y_nt != 0;
   if (t.nt >= 0) p.nontemporal = t.nt != 0;
