@@ -540,7 +540,10 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.slot32 = slot32;
   c.wide = wide;
   c.fin_rows = tn.csort_fin_rows;
-  c.dyn = tn.csort_dyn > 0;  // A/B first (r05)
+  // waves claim chunks from the workgroup's LDS queue: one process, 7
+  // rounds (profiles/r05c/ab_csort_dyn.jsonl): C5 106.9 -> 101.9 us median,
+  // c5r 107.3 -> 104.9, fp64 C5 flat (175.7 -> 174.7)
+  c.dyn = tn.csort_dyn != 0;
   c.m = m;
   c.lds_bytes = (int32_t)(slot_bytes * max_slots_used);
   c.blk_c = s.d_cs_blk_c;
