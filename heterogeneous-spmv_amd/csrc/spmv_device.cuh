@@ -265,6 +265,16 @@ struct XWin {
 // C forms the products into LDS; then the row sums.  PF (software
 // pipelining): the next chunk's stage A is issued between this chunk's
 // stage B and C, so its latency overlaps the gather and the sums.
+// First chunk of a group's first run, loaded by the caller ahead of time
+// (hspmv_csr3 early = 2: under the x-dictionary staging); valid only for
+// the run that starts at the group's first row.
+template <typename T, int U>
+struct PreChunk {
+  bool valid = false;
+  int32_t col[U];
+  T v[U];
+};
+
 template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD, bool GROUPS>
 __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, int32_t end,
                                           int32_t long_t, const ColSrc &cs,
@@ -272,7 +282,8 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
                                           const T *__restrict__ x,
                                           T *__restrict__ y, T *lds, int lane,
                                           const XWin<T> &win, bool y_nt, bool carry,
-                                          int32_t gbase, unsigned long long *ts = nullptr) {
+                                          int32_t gbase, unsigned long long *ts = nullptr,
+                                          const PreChunk<T, U> *pre = nullptr) {
   const int32_t row = g0 + lane;
   const bool valid = row < g1;
   const int32_t len = end - beg;
@@ -346,7 +357,15 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         }
       };
       if constexpr (PF) {
-        if (n_run > 0) stage_a(0, min(kWave * U, n_run) - 1);
+        if (pre && pre->valid && a == g0) {  // loaded by the caller (wave-uniform)
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            col[u] = pre->col[u];
+            v[u] = pre->v[u];
+          }
+        } else if (n_run > 0) {
+          stage_a(0, min(kWave * U, n_run) - 1);
+        }
       }
       for (int32_t c0 = 0; c0 < n_run; c0 += kWave * U) {
         const int32_t last = min(kWave * U, n_run - c0) - 1;
@@ -636,9 +655,40 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
   };
   auto first_end = [&]() { return align ? (r0 & ~(kWave - 1)) + kWave : r0 + kWave; };
   const bool pre = XD && early;
+  PreChunk<T, U> pc;
   if (pre && t < n_tasks) {
     task_bounds();
-    if (r0 < r1) group_bounds(rp, r0, min(first_end(), r1), lane, beg, end);
+    if (r0 < r1) {
+      group_bounds(rp, r0, min(first_end(), r1), lane, beg, end);
+      if constexpr (XD && PF) {
+        // early = 2: the first chunk's positions / values too (the same
+        // loads wave_rows' stage_a issues for the run at the group's first
+        // row), so their HBM round trip runs under the staging
+        if (early == 2) {
+          const int32_t g1 = min(first_end(), r1);
+          const bool valid = r0 + lane < g1;
+          const unsigned long long skip = __ballot(valid && end - beg > long_t);
+          const int32_t b = skip ? r0 + (__ffsll(skip) - 1) : g1;
+          if (b > r0) {
+            const int32_t kb = __builtin_amdgcn_readfirstlane(__shfl(beg, 0, kWave));
+            const int32_t ke = __builtin_amdgcn_readfirstlane(__shfl(end, b - 1 - r0, kWave));
+            const int32_t n_run = ke - kb;
+            if (n_run > 0) {
+              const gchar *cb = uniform_ptr(cs.c16 + kb);
+              const gchar *vb = uniform_ptr(val + kb);
+              const int32_t last = min(kWave * U, n_run) - 1;
+#pragma unroll
+              for (int u = 0; u < U; ++u) {
+                const uint32_t j = (uint32_t)min(u * kWave + lane, last);
+                pc.col[u] = (int32_t)ld_off<NT, uint16_t>(cb, j * 2u);
+                pc.v[u] = ld_off<NT, T>(vb, j * (uint32_t)sizeof(T));
+              }
+              pc.valid = true;
+            }
+          }
+        }
+      }
+    }
   }
   // XD: the W packed tasks of the block share one staged dictionary
   if constexpr (XD) stage_xdict<T, W * 64>(reinterpret_cast<T *>(xdyn), x, xd, blk, threadIdx.x);
@@ -677,7 +727,8 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
     wave_rows<T, NT, U, PF, C16, XW, XD, HSPMV_COOP_GROUPS != 0>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                         win, y_nt != 0, carry != 0, gbase, ts);
+                                         win, y_nt != 0, carry != 0, gbase, ts, &pc);
+    pc.valid = false;
     ts = nullptr;
     beg = nbeg;
     end = nend;

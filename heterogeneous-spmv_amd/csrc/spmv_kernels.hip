@@ -385,7 +385,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   // (bounds loaded ahead of the dictionary staging: C3 111.7 -> 111.0 us,
   // fp32 65.4 -> 64.4, c3h flat -- under the 2 % a change must earn;
   // profiles/r05c/ab_early_bounds.jsonl; A/B knob only)
-  p.early_bounds = t.early_bounds > 0 ? 1 : 0;
+  p.early_bounds = t.early_bounds > 0 ? (t.early_bounds >= 2 ? 2 : 1) : 0;
   if (t.pf >= 0) p.prefetch = t.pf != 0;  // A/B knobs (diagnostic builds only)
   if (t.y_nt >= 0) p.y_nt = t.y_nt != 0;
   if (t.nt >= 0) p.nontemporal = t.nt != 0;
