@@ -491,11 +491,20 @@ def self_launch(args, argv) -> int:
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     for k, v in RANK_ENV.items():
         env.setdefault(k, v)
+    import signal
     proc = subprocess.Popen(launch_command(argv, args.gpus, port), env=env, stdout=subprocess.PIPE,
                             text=True, bufsize=1)
-    for line in proc.stdout:
-        sys.stdout.write(line)
-        sys.stdout.flush()
+
+    def stop(signum, _frame):  # a timeout's SIGTERM reaches the ranks too
+        proc.send_signal(signum)
+
+    signal.signal(signal.SIGTERM, stop)
+    try:
+        for line in proc.stdout:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+    except KeyboardInterrupt:
+        proc.send_signal(signal.SIGINT)
     return proc.wait()
 
 
