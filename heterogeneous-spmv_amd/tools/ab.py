@@ -25,7 +25,7 @@ import torch  # noqa: E402,F401  (load order: torch's HIP runtime first)
 
 from hspmv import _lib, gen  # noqa: E402
 from hspmv.api import _KERNELS  # noqa: E402
-from sweep import build  # noqa: E402
+from auto_regret import build  # noqa: E402  (sweep.build + the planner zoo)
 
 
 def load(path):

@@ -329,9 +329,10 @@ def test_config_c5_powerlaw_csr3_fp32():
     columns make the gathers irregular, so AUTO runs the column-sorted row
     blocks (csort: fp64 row sums, rounded once): y is checked against the
     exact (fp64) sums to an fp32 rounding and against omp_spmv's fp32 sums
-    within their summation error.  The x-slab CSR-3 path (options x_slabs)
-    stays available and bitwise on short rows, and deterministic=1 keeps the
-    row kernels."""
+    within their summation error.  The x-slab path (options x_slabs) stays
+    available and bitwise on short rows -- AUTO streams its passes with
+    STREAM (C5's 64-row groups are balanced: slab_kernel_rule), the CSR3
+    tasks when forced -- and deterministic=1 keeps the row kernels."""
     A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32)
     maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
     x = gen.rand_x(A.n, 9).astype(np.float32)
@@ -352,9 +353,12 @@ def test_config_c5_powerlaw_csr3_fp32():
             assert np.all(np.abs(yi - y64) <= 2.0 ** -24 * np.abs(y64) + 1e-12 * absrow), it
             err = np.abs(yi.astype(np.float64) - y32.astype(np.float64))
             assert np.all(err <= (lens + 2) * 2.0 ** -23 * absrow + 1e-30), it
-    ys, info = gpu_spmv(A, x, maps, options={"x_slabs": 4})
-    assert info["kernel_name"] == "csr3" and info["x_slabs"] == 4
     ok = short_rows(A)
+    ys, info = gpu_spmv(A, x, maps, options={"x_slabs": 4})
+    assert info["kernel_name"] == "stream" and info["x_slabs"] == 4 and info["slab_kernel_rule"] == 2
+    assert np.array_equal(ys[ok].view(np.uint32), y32[ok].view(np.uint32))
+    ys, info = gpu_spmv(A, x, maps, kernel="csr3", options={"x_slabs": 4})
+    assert info["kernel_name"] == "csr3" and info["x_slabs"] == 4
     assert np.array_equal(ys[ok].view(np.uint32), y32[ok].view(np.uint32))
 
 
