@@ -99,7 +99,8 @@ def build(name: str):
         import sweep
         A, maps, desc = sweep.build("c5")
         return A.astype(np.float64), maps, desc.replace("fp32", "fp64")
-    raise ValueError(name)
+    import sweep  # the sweep's other configurations (c3m, c3s<a>x<b>, c4p<P>, ...)
+    return sweep.build(name)
 
 
 def variants(A, maps, deterministic=False):
