@@ -72,6 +72,22 @@ constexpr int kWave = 64;
 constexpr int kSerialMax = HSPMV_SERIAL_MAX;  // longest row summed serially by one lane
 constexpr int kNumXcd = 8;
 
+// A wave's product buffer holds chunk position i at lds_ix(i) = i + i / 32:
+// one pad element per 32, so that the lanes of an ordered sum -- each
+// walking its own row, rows one row length apart -- do not meet in one LDS
+// bank.  Without it rows of 32 nonzeros put every lane of a chunk on one
+// bank (fp32: 32-way; fp64 rows of 32: 8-way per 256-nonzero chunk), and
+// the ordered sums were 40 % of the dense-32x32-block matrix's time
+// (HSPMV_DIAG 1 ablation, profiles/r05h/ab_blocks32_ablation.jsonl).
+#ifndef HSPMV_LDS_PAD
+#define HSPMV_LDS_PAD 1
+#endif
+__device__ __forceinline__ int32_t lds_ix(int32_t i) { return HSPMV_LDS_PAD ? i + (i >> 5) : i; }
+template <int U>
+constexpr int wave_lds() {  // elements of one wave's product buffer
+  return kWave * U + (HSPMV_LDS_PAD ? 2 * U : 0);
+}
+
 template <bool NT, typename T>
 __device__ __forceinline__ T ldg(const T *p) {
   if constexpr (NT)
@@ -210,18 +226,21 @@ __device__ __forceinline__ int64_t sload_i64(const void *p, uint64_t byte_off) {
 // sequence, so the rounding is omp_spmv's.
 // (An 8-wide batch for the dictionary kernels measured flat on C3, -0.4 %;
 // 8-wide clamped batches everywhere slower: C3 +13 %, honeycomb +5 %.)
+// lds holds chunk position i (nonzero c + i) at lds_ix(i).
 template <typename T>
-__device__ __forceinline__ T ordered_sum(T acc, const T *lds, int32_t lo, int32_t hi) {
+__device__ __forceinline__ T ordered_sum(T acc, const T *lds, int32_t c, int32_t lo, int32_t hi) {
   int32_t k = lo;
   for (; k + 4 <= hi; k += 4) {
-    const T a0 = lds[k], a1 = lds[k + 1], a2 = lds[k + 2], a3 = lds[k + 3];
+    const T a0 = lds[lds_ix(k - c)], a1 = lds[lds_ix(k + 1 - c)], a2 = lds[lds_ix(k + 2 - c)],
+            a3 = lds[lds_ix(k + 3 - c)];
     acc = acc + a0;
     acc = acc + a1;
     acc = acc + a2;
     acc = acc + a3;
   }
   if (k < hi) {  // the last 1-3 in one LDS round trip (clamped reads, selected adds)
-    const T a0 = lds[k], a1 = lds[min(k + 1, hi - 1)], a2 = lds[min(k + 2, hi - 1)];
+    const T a0 = lds[lds_ix(k - c)], a1 = lds[lds_ix(min(k + 1, hi - 1) - c)],
+            a2 = lds[lds_ix(min(k + 2, hi - 1) - c)];
     acc = acc + a0;
     if (k + 1 < hi) acc = acc + a1;
     if (k + 2 < hi) acc = acc + a2;
@@ -400,13 +419,13 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         if (c0 == 0) HSPMV_TRACE(ts, 3, diag_stamp());
 #endif
 #pragma unroll
-        for (int u = 0; u < U; ++u) lds[u * kWave + lane] = vv[u] * xv[u];
+        for (int u = 0; u < U; ++u) lds[lds_ix(u * kWave + lane)] = vv[u] * xv[u];
         wave_sync();
         const int32_t c = kb + c0;
         if constexpr ((HSPMV_DIAG & 1) != 0) {
-          if (mine && max(beg, c) < min(end, c + last + 1)) acc += lds[max(beg, c) - c];
+          if (mine && max(beg, c) < min(end, c + last + 1)) acc += lds[lds_ix(max(beg, c) - c)];
         } else {
-          if (mine) acc = ordered_sum(acc, lds - c, max(beg, c), min(end, c + last + 1));
+          if (mine) acc = ordered_sum(acc, lds, c, max(beg, c), min(end, c + last + 1));
         }
         // only the cooperative rows this chunk touches (rows are contiguous:
         // the others would add nothing), bounds by readlane (scalar)
@@ -437,7 +456,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
             const int32_t lo = g == 0 ? lq[0] : (g == 1 ? lq[1] : (g == 2 ? lq[2] : lq[3]));
             const int32_t hi = g == 0 ? hq[0] : (g == 1 ? hq[1] : (g == 2 ? hq[2] : hq[3]));
             T s = T(0);
-            for (int32_t k = lo + gl; k < hi; k += 16) s += lds[k - c];
+            for (int32_t k = lo + gl; k < hi; k += 16) s += lds[lds_ix(k - c)];
             s = row16_sum_dpp(s);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -454,7 +473,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
           const int32_t hi = min(__builtin_amdgcn_readlane(end, r), c + last + 1);
           if (lo < hi) {  // wave-uniform
             T s = T(0);
-            for (int32_t k = lo + lane; k < hi; k += kWave) s += lds[k - c];
+            for (int32_t k = lo + lane; k < hi; k += kWave) s += lds[lds_ix(k - c)];
             s = wave_sum_dpp(s);
             if (lane == r) acc += s;
           }
@@ -569,7 +588,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
     const int32_t *__restrict__ rp, ColSrc cs, const int2 *__restrict__ xwin, XDict xd,
     const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
   static_assert(!XD || W == 4, "dictionaries are planned for 256-row blocks");
-  __shared__ T lds[W * kWave * U];
+  __shared__ T lds[W * wave_lds<U>()];
   __shared__ T xlds[XW ? W * kXWin : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char xdyn[];  // XD: the block's xs
   const int wid = threadIdx.x >> 6;
@@ -581,7 +600,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
   int64_t g0 = (blk * W + wid) * (int64_t)groups * kWave;
   if (g0 >= m) return;  // wave-uniform
   const int64_t gend = min<int64_t>(g0 + (int64_t)groups * kWave, m);
-  T *my = lds + wid * kWave * U;
+  T *my = lds + wid * wave_lds<U>();
   unsigned long long *ts = nullptr;
 #if (HSPMV_DIAG & 8)
   const int64_t wv = blk * W + wid;
@@ -628,7 +647,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t early, const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin, XDict xd,
     const int32_t *__restrict__ rp, ColSrc cs, const T *__restrict__ val,
     const T *__restrict__ x, T *__restrict__ y) {
-  __shared__ T lds[W * kWave * U];
+  __shared__ T lds[W * wave_lds<U>()];
   __shared__ T xlds[XW ? W * kXWin : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char xdyn[];  // XD: the block's xs
   const int wid = threadIdx.x >> 6;
@@ -698,7 +717,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
 #endif
   if (!pre) task_bounds();
   if (r0 >= r1) return;
-  T *my = lds + wid * kWave * U;
+  T *my = lds + wid * wave_lds<U>();
   // group-base columns: one base per packed task
   int32_t gbase = 0;
   if constexpr (C16 == 2) gbase = (int32_t)sload_i64(cs.cbase, (uint64_t)t * 4u);
