@@ -431,6 +431,7 @@ static int fill_info(hspmv_handle *h, hspmv_info *out) {
   out->rccl_version = h->rccl_version;
   out->slab_kernel_rule = s.heavy_frac < 0 ? 0 : (s.A.slab_stream ? 2 : 1);
   out->heavy_group_frac = s.heavy_frac < 0 ? 0.0 : s.heavy_frac;
+  out->lds_pad = s.plan.lds_pad ? 1 : 0;
   for (auto &sh : h->shards)
     if (sh.plan.kernel == kCsort) {
       out->csort_chunks += sh.csort_chunks;

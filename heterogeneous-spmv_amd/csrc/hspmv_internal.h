@@ -36,6 +36,7 @@ struct DevCSR {
                               // blocks); the SSR plan: ssr_waves() per super-super-row
   bool has_csort = false;     // column-sorted row blocks were built (irregular gathers)
   bool slab_stream = false;   // x-slab passes with CSR-3 tasks: AUTO runs STREAM (slab_kernel_rule)
+  int32_t serial_len = 0;     // median length of the rows summed serially (<= kSerialMax), 0 = none
 };
 
 // Planner choices of one handle.  The first block mirrors hspmv_options
@@ -77,6 +78,7 @@ struct Tuning {
   int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4)
   int csort_dyn = -1;                    // chunks claimed from an LDS queue (-1: the library's choice)
   int early_bounds = -1;                 // CSR3 + x dictionaries: bounds before the staging (-1: default)
+  int lds_pad = -1;                      // STREAM padded product buffers (-1: by row length, 0 off, 1 on)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
 };
@@ -182,6 +184,7 @@ struct LaunchPlan {
   int32_t groups = 1;      // STREAM: 64-row groups per wave (next group's rp prefetched)
   int32_t carry = 0;       // STREAM/CSR3: rows start from y (x-slab passes after the first)
   int32_t early_bounds = 0; // CSR3 + x dictionaries: task / row bounds loaded before the staging
+  bool lds_pad = false;     // STREAM: bank-padded product buffers (spmv_device.cuh lds_ix)
   int64_t blocks = 0;
 };
 

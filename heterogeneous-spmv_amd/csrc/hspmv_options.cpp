@@ -85,6 +85,7 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_CSORT_FIN_ROWS", &t->csort_fin_rows);
   geti("HSPMV_CSORT_DYN", &t->csort_dyn);
   geti("HSPMV_EARLY_BOUNDS", &t->early_bounds);
+  geti("HSPMV_LDS_PAD", &t->lds_pad);
   geti("HSPMV_STREAM_W", &t->stream_waves);
   geti("HSPMV_PLACEMENT", &t->placement_trials);
   geti("HSPMV_SSR_ALIGN", &t->ssr_align);

@@ -627,6 +627,22 @@ void slab_kernel_rule(Shard &s, const int32_t *rp, int64_t m, unsigned flags) {
 // kernels.
 int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void *val, int64_t m,
                      int64_t n, int dtype, unsigned flags) {
+  // the typical serially summed row (median length of the rows of 1..40
+  // nonzeros, spmv_device.cuh kSerialMax): the planner's LDS bank rule
+  {
+    constexpr int kSerial = 40;
+    int64_t hist[kSerial + 1] = {0}, tot = 0;
+    for (int64_t r = 0; r < m; ++r) {
+      const int64_t len = rp[r + 1] - rp[r];
+      if (len >= 1 && len <= kSerial) {
+        ++hist[len];
+        ++tot;
+      }
+    }
+    int32_t med = 0;
+    for (int64_t acc = 0; med < kSerial && 2 * acc < tot;) acc += hist[++med];
+    s.A.serial_len = tot ? med : 0;
+  }
   int waves = 4;
   build_tasks(rp, m, s.A.n_ssr > 0 ? &s.h_inner : nullptr, s.A.n_ssr > 0 ? &s.h_outer : nullptr,
               flags, s.tune, s.h_tasks, &waves);

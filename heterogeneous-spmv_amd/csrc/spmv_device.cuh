@@ -72,20 +72,21 @@ constexpr int kWave = 64;
 constexpr int kSerialMax = HSPMV_SERIAL_MAX;  // longest row summed serially by one lane
 constexpr int kNumXcd = 8;
 
-// A wave's product buffer holds chunk position i at lds_ix(i) = i + i / 32:
-// one pad element per 32, so that the lanes of an ordered sum -- each
-// walking its own row, rows one row length apart -- do not meet in one LDS
-// bank.  Without it rows of 32 nonzeros put every lane of a chunk on one
-// bank (fp32: 32-way; fp64 rows of 32: 8-way per 256-nonzero chunk), and
-// the ordered sums were 40 % of the dense-32x32-block matrix's time
-// (HSPMV_DIAG 1 ablation, profiles/r05h/ab_blocks32_ablation.jsonl).
-#ifndef HSPMV_LDS_PAD
-#define HSPMV_LDS_PAD 1
-#endif
-__device__ __forceinline__ int32_t lds_ix(int32_t i) { return HSPMV_LDS_PAD ? i + (i >> 5) : i; }
-template <int U>
+// PAD: a wave's product buffer holds chunk position i at lds_ix(i) = i + i /
+// 32 -- one pad element per 32 -- so that the lanes of an ordered sum, each
+// walking its own row with rows one row length apart, do not meet in one
+// LDS bank.  Rows of 32 nonzeros put every lane of a chunk on one bank
+// (fp32 32-way; fp64 8-way per 256-nonzero chunk), and the ordered sums were
+// 40 % of the dense-32x32-block matrix's time (HSPMV_DIAG 1 ablation,
+// profiles/r05h/ab_blocks32_ablation.jsonl).  The index math and the bigger
+// buffer cost latency and LDS elsewhere (C3 fp32 +8 %, C4 fp32 +8 % with
+// padding everywhere, profiles/r05j/ab_lds_pad.jsonl), so the planner pads
+// only STREAM launches whose rows are conflicting (LaunchPlan.lds_pad).
+template <bool PAD>
+__device__ __forceinline__ int32_t lds_ix(int32_t i) { return PAD ? i + (i >> 5) : i; }
+template <int U, bool PAD>
 constexpr int wave_lds() {  // elements of one wave's product buffer
-  return kWave * U + (HSPMV_LDS_PAD ? 2 * U : 0);
+  return kWave * U + (PAD ? 2 * U : 0);
 }
 
 template <bool NT, typename T>
@@ -227,20 +228,20 @@ __device__ __forceinline__ int64_t sload_i64(const void *p, uint64_t byte_off) {
 // (An 8-wide batch for the dictionary kernels measured flat on C3, -0.4 %;
 // 8-wide clamped batches everywhere slower: C3 +13 %, honeycomb +5 %.)
 // lds holds chunk position i (nonzero c + i) at lds_ix(i).
-template <typename T>
+template <bool PAD, typename T>
 __device__ __forceinline__ T ordered_sum(T acc, const T *lds, int32_t c, int32_t lo, int32_t hi) {
   int32_t k = lo;
   for (; k + 4 <= hi; k += 4) {
-    const T a0 = lds[lds_ix(k - c)], a1 = lds[lds_ix(k + 1 - c)], a2 = lds[lds_ix(k + 2 - c)],
-            a3 = lds[lds_ix(k + 3 - c)];
+    const T a0 = lds[lds_ix<PAD>(k - c)], a1 = lds[lds_ix<PAD>(k + 1 - c)], a2 = lds[lds_ix<PAD>(k + 2 - c)],
+            a3 = lds[lds_ix<PAD>(k + 3 - c)];
     acc = acc + a0;
     acc = acc + a1;
     acc = acc + a2;
     acc = acc + a3;
   }
   if (k < hi) {  // the last 1-3 in one LDS round trip (clamped reads, selected adds)
-    const T a0 = lds[lds_ix(k - c)], a1 = lds[lds_ix(min(k + 1, hi - 1) - c)],
-            a2 = lds[lds_ix(min(k + 2, hi - 1) - c)];
+    const T a0 = lds[lds_ix<PAD>(k - c)], a1 = lds[lds_ix<PAD>(min(k + 1, hi - 1) - c)],
+            a2 = lds[lds_ix<PAD>(min(k + 2, hi - 1) - c)];
     acc = acc + a0;
     if (k + 1 < hi) acc = acc + a1;
     if (k + 2 < hi) acc = acc + a2;
@@ -294,7 +295,7 @@ struct PreChunk {
   T v[U];
 };
 
-template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD, bool GROUPS>
+template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD, bool GROUPS, bool PAD = false>
 __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, int32_t end,
                                           int32_t long_t, const ColSrc &cs,
                                           const T *__restrict__ val,
@@ -419,13 +420,13 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         if (c0 == 0) HSPMV_TRACE(ts, 3, diag_stamp());
 #endif
 #pragma unroll
-        for (int u = 0; u < U; ++u) lds[lds_ix(u * kWave + lane)] = vv[u] * xv[u];
+        for (int u = 0; u < U; ++u) lds[lds_ix<PAD>(u * kWave + lane)] = vv[u] * xv[u];
         wave_sync();
         const int32_t c = kb + c0;
         if constexpr ((HSPMV_DIAG & 1) != 0) {
-          if (mine && max(beg, c) < min(end, c + last + 1)) acc += lds[lds_ix(max(beg, c) - c)];
+          if (mine && max(beg, c) < min(end, c + last + 1)) acc += lds[lds_ix<PAD>(max(beg, c) - c)];
         } else {
-          if (mine) acc = ordered_sum(acc, lds, c, max(beg, c), min(end, c + last + 1));
+          if (mine) acc = ordered_sum<PAD>(acc, lds, c, max(beg, c), min(end, c + last + 1));
         }
         // only the cooperative rows this chunk touches (rows are contiguous:
         // the others would add nothing), bounds by readlane (scalar)
@@ -456,7 +457,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
             const int32_t lo = g == 0 ? lq[0] : (g == 1 ? lq[1] : (g == 2 ? lq[2] : lq[3]));
             const int32_t hi = g == 0 ? hq[0] : (g == 1 ? hq[1] : (g == 2 ? hq[2] : hq[3]));
             T s = T(0);
-            for (int32_t k = lo + gl; k < hi; k += 16) s += lds[lds_ix(k - c)];
+            for (int32_t k = lo + gl; k < hi; k += 16) s += lds[lds_ix<PAD>(k - c)];
             s = row16_sum_dpp(s);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -473,7 +474,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
           const int32_t hi = min(__builtin_amdgcn_readlane(end, r), c + last + 1);
           if (lo < hi) {  // wave-uniform
             T s = T(0);
-            for (int32_t k = lo + lane; k < hi; k += kWave) s += lds[lds_ix(k - c)];
+            for (int32_t k = lo + lane; k < hi; k += kWave) s += lds[lds_ix<PAD>(k - c)];
             s = wave_sum_dpp(s);
             if (lane == r) acc += s;
           }
@@ -582,13 +583,13 @@ __device__ __forceinline__ void stage_xdict(T *xs, const T *__restrict__ x, cons
 // w * groups * 64, loading the next group's row pointers before streaming
 // the current one.  XW: groups whose x window (xwin[g] = {lo, w}) fits
 // kXWin entries gather from an LDS copy of it.
-template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD, int W = 4>
+template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD, int W = 4, bool PAD = false>
 __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
     int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups, int32_t y_nt, int32_t carry,
     const int32_t *__restrict__ rp, ColSrc cs, const int2 *__restrict__ xwin, XDict xd,
     const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
   static_assert(!XD || W == 4, "dictionaries are planned for 256-row blocks");
-  __shared__ T lds[W * wave_lds<U>()];
+  __shared__ T lds[W * wave_lds<U, PAD>()];
   __shared__ T xlds[XW ? W * kXWin : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char xdyn[];  // XD: the block's xs
   const int wid = threadIdx.x >> 6;
@@ -600,7 +601,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
   int64_t g0 = (blk * W + wid) * (int64_t)groups * kWave;
   if (g0 >= m) return;  // wave-uniform
   const int64_t gend = min<int64_t>(g0 + (int64_t)groups * kWave, m);
-  T *my = lds + wid * wave_lds<U>();
+  T *my = lds + wid * wave_lds<U, PAD>();
   unsigned long long *ts = nullptr;
 #if (HSPMV_DIAG & 8)
   const int64_t wv = blk * W + wid;
@@ -631,7 +632,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
     if (g1 < gend) group_bounds(rp, g1, (int32_t)min<int64_t>(g1 + kWave, gend), lane, nbeg, nend);
     int32_t gbase = 0;
     if constexpr (C16 == 2) gbase = (int32_t)sload_i64(cs.cbase, (uint64_t)(g0 / kWave) * 4u);
-    wave_rows<T, NT, U, PF, C16, XW, XD, false>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my,
+    wave_rows<T, NT, U, PF, C16, XW, XD, false, PAD>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my,
                                          lane, win, y_nt != 0, carry != 0, gbase, ts);
     ts = nullptr;  // trace the first group only
     if (g1 >= gend) break;
@@ -647,7 +648,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t early, const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin, XDict xd,
     const int32_t *__restrict__ rp, ColSrc cs, const T *__restrict__ val,
     const T *__restrict__ x, T *__restrict__ y) {
-  __shared__ T lds[W * wave_lds<U>()];
+  __shared__ T lds[W * wave_lds<U, false>()];
   __shared__ T xlds[XW ? W * kXWin : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char xdyn[];  // XD: the block's xs
   const int wid = threadIdx.x >> 6;
@@ -717,7 +718,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
 #endif
   if (!pre) task_bounds();
   if (r0 >= r1) return;
-  T *my = lds + wid * wave_lds<U>();
+  T *my = lds + wid * wave_lds<U, false>();
   // group-base columns: one base per packed task
   int32_t gbase = 0;
   if constexpr (C16 == 2) gbase = (int32_t)sload_i64(cs.cbase, (uint64_t)t * 4u);
@@ -773,41 +774,34 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
   const unsigned dyn = XD ? (unsigned)dp.xd_lds_bytes + (unsigned)p.dyn_lds : (unsigned)p.dyn_lds;
   if (p.kernel == kStream) {
     const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
-    if constexpr (XD)
-      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, false, false, true>),
-                         dim3((unsigned)p.blocks), dim3(256), dyn, st, A.m, dp.long_t,
-                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
-                         xw, xd, val, x, y);
-    else if (p.waves_per_block == 1 && xw)
-      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true, false, 1>),
-                         dim3((unsigned)p.blocks), dim3(64), dyn, st, A.m, dp.long_t,
-                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
-                         xw, xd, val, x, y);
-    else if (p.waves_per_block == 1)
-      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false, false, 1>),
-                         dim3((unsigned)p.blocks), dim3(64), dyn, st, A.m, dp.long_t,
-                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
-                         xw, xd, val, x, y);
-    else if (p.waves_per_block != 4 && xw)
-      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true, false, 2>),
-                         dim3((unsigned)p.blocks), dim3(128), dyn, st, A.m, dp.long_t,
-                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
-                         xw, xd, val, x, y);
-    else if (p.waves_per_block != 4)
-      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false, false, 2>),
-                         dim3((unsigned)p.blocks), dim3(128), dyn, st, A.m, dp.long_t,
-                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
-                         xw, xd, val, x, y);
-    else if (xw)
-      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, true, false>),
-                         dim3((unsigned)p.blocks), dim3(256), dyn, st, A.m, dp.long_t,
-                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
-                         xw, xd, val, x, y);
-    else
-      hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C16, false, false>),
-                         dim3((unsigned)p.blocks), dim3(256), dyn, st, A.m, dp.long_t,
-                         (uint32_t)p.xcd_chunk, (int32_t)p.groups, (int32_t)p.y_nt, p.carry, A.row_ptr, cs,
-                         xw, xd, val, x, y);
+#define HSPMV_STREAM(C, XW, XDX, W, PAD)                                                            \
+  hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C, XW, XDX, W, PAD>), dim3((unsigned)p.blocks), \
+                     dim3(W * 64), dyn, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk, (int32_t)p.groups,  \
+                     (int32_t)p.y_nt, p.carry, A.row_ptr, cs, xw, xd, val, x, y)
+    if constexpr (XD) {
+      HSPMV_STREAM(false, false, true, 4, false);
+      return;
+    }
+    // padded product buffers (LaunchPlan.lds_pad): conflicting row lengths,
+    // no prefetch variant (the planner never pairs them)
+    if constexpr (!PF) {
+      if (p.lds_pad) {
+        if (p.waves_per_block == 1 && xw) HSPMV_STREAM(C16, true, false, 1, true);
+        else if (p.waves_per_block == 1) HSPMV_STREAM(C16, false, false, 1, true);
+        else if (p.waves_per_block != 4 && xw) HSPMV_STREAM(C16, true, false, 2, true);
+        else if (p.waves_per_block != 4) HSPMV_STREAM(C16, false, false, 2, true);
+        else if (xw) HSPMV_STREAM(C16, true, false, 4, true);
+        else HSPMV_STREAM(C16, false, false, 4, true);
+        return;
+      }
+    }
+    if (p.waves_per_block == 1 && xw) HSPMV_STREAM(C16, true, false, 1, false);
+    else if (p.waves_per_block == 1) HSPMV_STREAM(C16, false, false, 1, false);
+    else if (p.waves_per_block != 4 && xw) HSPMV_STREAM(C16, true, false, 2, false);
+    else if (p.waves_per_block != 4) HSPMV_STREAM(C16, false, false, 2, false);
+    else if (xw) HSPMV_STREAM(C16, true, false, 4, false);
+    else HSPMV_STREAM(C16, false, false, 4, false);
+#undef HSPMV_STREAM
     return;
   }
   {

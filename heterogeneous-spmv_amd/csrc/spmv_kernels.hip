@@ -386,6 +386,19 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   // fp32 65.4 -> 64.4, c3h flat -- under the 2 % a change must earn;
   // profiles/r05c/ab_early_bounds.jsonl; A/B knob only)
   p.early_bounds = t.early_bounds > 0 ? (t.early_bounds >= 2 ? 2 : 1) : 0;
+  // Bank-padded product buffers (STREAM, no dictionaries, no prefetch): when
+  // the typical serially summed row is a multiple of 16 LDS words long
+  // (fp32 rows of 16 / 32, fp64 rows of 8 / 16 / 24 / 32 ...), the lanes
+  // walking those rows hit at most two banks.  Dense 32x32 blocks: fp64
+  // 129.6 -> 95.1 us, fp32 99.6 -> 67.1; fp64 rows of 24: 103.2 -> 95.9;
+  // fp32 rows of 24 (8-word multiples) lose 3 % padded, so they are left
+  // alone (profiles/r05j/ab_lds_pad.jsonl).
+  {
+    const int words = A.serial_len * (dtype == 1 ? 2 : 1);
+    const bool conflicting = words > 0 && (words % 16) == 0;
+    p.lds_pad = p.kernel == kStream && !A.has_xdict && !p.prefetch && conflicting;
+    if (t.lds_pad >= 0) p.lds_pad = p.kernel == kStream && !A.has_xdict && !p.prefetch && t.lds_pad > 0;
+  }
   if (t.pf >= 0) p.prefetch = t.pf != 0;  // A/B knobs (diagnostic builds only)
   if (t.y_nt >= 0) p.y_nt = t.y_nt != 0;
   if (t.nt >= 0) p.nontemporal = t.nt != 0;

@@ -119,7 +119,7 @@ class Info(C.Structure):
                 ("csort_slot_bytes", C.c_int32), ("csort_row_blocks", C.c_int32),
                 ("rccl_version", C.c_int32), ("reserved0", C.c_int32),
                 ("csort_chunks", C.c_int64), ("csort_seg_chunks", C.c_int64),
-                ("slab_kernel_rule", C.c_int32), ("reserved1", C.c_int32),
+                ("slab_kernel_rule", C.c_int32), ("lds_pad", C.c_int32),
                 ("heavy_group_frac", C.c_double)]
 
 

@@ -184,7 +184,9 @@ typedef struct {
                                64-row groups (> 2048 nonzeros) hold >= 1/8
                                of the nonzeros; 2 = STREAM groups (balanced
                                groups); 0 = the rule did not apply          */
-  int32_t reserved1;
+  int32_t lds_pad;          /* STREAM: 1 = bank-padded LDS product buffers
+                               (the typical row of <= 40 nonzeros is a
+                               multiple of 16 LDS words long)              */
   double heavy_group_frac;  /* the share of nonzeros in heavy 64-row groups
                                the rule read (0 when it did not apply)     */
 } hspmv_info;

@@ -126,3 +126,32 @@ def test_csr3_maps_with_dense_super_rows():
     y, info = run(A, x, maps)
     assert info["kernel_name"] == "csr3" and info["wave_tasks"] >= A.nnz // 2048
     check(A, x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_bank_padded_product_buffers_on_32_nonzero_rows(dtype):
+    """Rows of 32 nonzeros (dense 32 x 32 diagonal blocks) make every lane of
+    an ordered sum walk the same LDS bank, so STREAM pads its product buffers
+    (hspmv_info.lds_pad); rows of 27 do not.  Padded or not, y is the
+    reference's left-to-right sum bit for bit."""
+    m, b = 300_000, 32
+    rows = np.arange(m, dtype=np.int64)
+    ci = ((rows // b) * b)[:, None] + np.arange(b, dtype=np.int64)[None, :]
+    rng = np.random.default_rng(3)
+    rp = np.arange(0, m * b + 1, b, dtype=np.int64).astype(np.int32)
+    A = hspmv.CsrMatrix(m, m, rp, ci.reshape(-1).astype(np.int32), rng.uniform(-1, 1, m * b).astype(dtype))
+    x = gen.rand_x(A.n, 4).astype(dtype)
+    ref = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    with hspmv.SpMV(A, kernel="stream") as op:
+        y = op(x)
+        assert op.info["lds_pad"] == 1
+    assert np.array_equal(y.view(np.uint8), ref.view(np.uint8))
+    S = gen.stencil27(40).astype(dtype)  # 27-nonzero rows: no padding
+    xs = gen.rand_x(S.n, 5).astype(dtype)
+    with hspmv.SpMV(S, kernel="stream") as op:
+        ys = op(xs)
+        assert op.info["lds_pad"] == 0
+    short = np.diff(S.row_ptr) <= 40
+    rs = oracle.spmv(S.row_ptr, S.col_idx, S.val, xs)
+    assert np.array_equal(ys[short].view(np.uint8), rs[short].view(np.uint8))
