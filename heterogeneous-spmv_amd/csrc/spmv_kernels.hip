@@ -386,7 +386,7 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   // fp32 65.4 -> 64.4, c3h flat -- under the 2 % a change must earn;
   // profiles/r05c/ab_early_bounds.jsonl; A/B knob only)
   p.early_bounds = t.early_bounds > 0 ? (t.early_bounds >= 2 ? 2 : 1) : 0;
-  // Bank-padded product buffers (STREAM, no dictionaries, no prefetch): when
+  // Bank-padded product buffers (STREAM, no prefetch): when
   // the typical serially summed row is a multiple of 16 LDS words long
   // (fp32 rows of 16 / 32, fp64 rows of 8 / 16 / 24 / 32 ...), the lanes
   // walking those rows hit at most two banks.  Dense 32x32 blocks: fp64
@@ -396,8 +396,8 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   {
     const int words = A.serial_len * (dtype == 1 ? 2 : 1);
     const bool conflicting = words > 0 && (words % 16) == 0;
-    p.lds_pad = p.kernel == kStream && !A.has_xdict && !p.prefetch && conflicting;
-    if (t.lds_pad >= 0) p.lds_pad = p.kernel == kStream && !A.has_xdict && !p.prefetch && t.lds_pad > 0;
+    p.lds_pad = p.kernel == kStream && !p.prefetch && conflicting;
+    if (t.lds_pad >= 0) p.lds_pad = p.kernel == kStream && !p.prefetch && t.lds_pad > 0;
   }
   if (t.pf >= 0) p.prefetch = t.pf != 0;  // A/B knobs (diagnostic builds only)
   if (t.y_nt >= 0) p.y_nt = t.y_nt != 0;
