@@ -111,7 +111,7 @@ def test_self_launch_spawns_the_launcher_without_touching_the_gpu():
     assert cmd[-4:] == ["--gpus", "4", "--steps", "7"] and cmd[-5].endswith("bench.py")
 
 
-def test_cpu_c1_leg_times_configs0(monkeypatch):
+def test_cpu_c1_leg_times_configs0():
     """The cpu_c1 leg: configs[0]'s matrix (nnz = 4,996,000), fp64, x = 1 and
     x = rand:42, static and guided, TimeMin/Max/Avg and GFLOP/s from TimeMin."""
     sys.path.insert(0, str(REPO))
