@@ -105,7 +105,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     std::vector<int64_t> colcnt((size_t)n + 1, 0);
     for (int64_t k = 0; k < rp[m]; ++k) ++colcnt[(size_t)col[k]];
     const double nb_part = (double)std::max<int64_t>(1, (int64_t)cus * bpc / H);
-    const double wcol = kSweepPerRowBlock * nb_part * (dtype == HSPMV_F64 ? 2.0 * 8.0 / 12.0 : 1.0);
+    const double wsw = tn.csort_sweep_w > 0 ? tn.csort_sweep_w : kSweepPerRowBlock;
+    const double wcol = wsw * nb_part * (dtype == HSPMV_F64 ? 2.0 * 8.0 / 12.0 : 1.0);
     const double tot = (double)rp[m] + wcol * (double)n;
     double acc = 0.0;
     int64_t c = 0;

@@ -77,6 +77,7 @@ struct Tuning {
   int csort_balance = 0;                 // -1: equal-width column parts, nnz-balanced rows (r03)
   int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4)
   int csort_dyn = -1;                    // chunks claimed from an LDS queue (-1: the library's choice)
+  double csort_sweep_w = 0;              // column-part cost of a column per row block (0: kSweepPerRowBlock)
   int early_bounds = -1;                 // CSR3 + x dictionaries: bounds before the staging (-1: default)
   int lds_pad = -1;                      // STREAM padded product buffers (-1: by row length, 0 off, 1 on)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
