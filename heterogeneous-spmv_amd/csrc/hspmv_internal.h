@@ -78,7 +78,6 @@ struct Tuning {
   int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4)
   int csort_dyn = -1;                    // chunks claimed from an LDS queue (-1: the library's choice)
   double csort_sweep_w = 0;              // column-part cost of a column per row block (0: kSweepPerRowBlock)
-  int early_bounds = -1;                 // CSR3 + x dictionaries: bounds before the staging (-1: default)
   int lds_pad = -1;                      // STREAM padded product buffers (-1: by row length, 0 off, 1 on)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
@@ -184,7 +183,6 @@ struct LaunchPlan {
   int32_t xcd_chunk = 1;   // blocks per XCD turn (1 = dispatch order; see xcd_chunk_remap)
   int32_t groups = 1;      // STREAM: 64-row groups per wave (next group's rp prefetched)
   int32_t carry = 0;       // STREAM/CSR3: rows start from y (x-slab passes after the first)
-  int32_t early_bounds = 0; // CSR3 + x dictionaries: task / row bounds loaded before the staging
   bool lds_pad = false;     // STREAM: bank-padded product buffers (spmv_device.cuh lds_ix)
   int64_t blocks = 0;
 };

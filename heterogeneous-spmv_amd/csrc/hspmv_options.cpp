@@ -85,7 +85,6 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_CSORT_FIN_ROWS", &t->csort_fin_rows);
   geti("HSPMV_CSORT_DYN", &t->csort_dyn);
   if (const char *e = getenv("HSPMV_CSORT_SWEEP")) t->csort_sweep_w = atof(e);
-  geti("HSPMV_EARLY_BOUNDS", &t->early_bounds);
   geti("HSPMV_LDS_PAD", &t->lds_pad);
   geti("HSPMV_STREAM_W", &t->stream_waves);
   geti("HSPMV_PLACEMENT", &t->placement_trials);

@@ -285,16 +285,6 @@ struct XWin {
 // C forms the products into LDS; then the row sums.  PF (software
 // pipelining): the next chunk's stage A is issued between this chunk's
 // stage B and C, so its latency overlaps the gather and the sums.
-// First chunk of a group's first run, loaded by the caller ahead of time
-// (hspmv_csr3 early = 2: under the x-dictionary staging); valid only for
-// the run that starts at the group's first row.
-template <typename T, int U>
-struct PreChunk {
-  bool valid = false;
-  int32_t col[U];
-  T v[U];
-};
-
 template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD, bool GROUPS, bool PAD = false>
 __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, int32_t end,
                                           int32_t long_t, const ColSrc &cs,
@@ -302,8 +292,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
                                           const T *__restrict__ x,
                                           T *__restrict__ y, T *lds, int lane,
                                           const XWin<T> &win, bool y_nt, bool carry,
-                                          int32_t gbase, unsigned long long *ts = nullptr,
-                                          const PreChunk<T, U> *pre = nullptr) {
+                                          int32_t gbase, unsigned long long *ts = nullptr) {
   const int32_t row = g0 + lane;
   const bool valid = row < g1;
   const int32_t len = end - beg;
@@ -377,15 +366,7 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
         }
       };
       if constexpr (PF) {
-        if (pre && pre->valid && a == g0) {  // loaded by the caller (wave-uniform)
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            col[u] = pre->col[u];
-            v[u] = pre->v[u];
-          }
-        } else if (n_run > 0) {
-          stage_a(0, min(kWave * U, n_run) - 1);
-        }
+        if (n_run > 0) stage_a(0, min(kWave * U, n_run) - 1);
       }
       for (int32_t c0 = 0; c0 < n_run; c0 += kWave * U) {
         const int32_t last = min(kWave * U, n_run - c0) - 1;
@@ -645,7 +626,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
 template <typename T, bool NT, int U, bool PF, int C16, int W, bool XW, bool XD>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, int32_t y_nt, int32_t carry, int32_t align,
-    int32_t early, const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin, XDict xd,
+    const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin, XDict xd,
     const int32_t *__restrict__ rp, ColSrc cs, const T *__restrict__ val,
     const T *__restrict__ x, T *__restrict__ y) {
   __shared__ T lds[W * wave_lds<U, false>()];
@@ -662,61 +643,20 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     bt[7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
   }
 #endif
-  const int64_t t = blk * W + wid;
-  // early (XD): the task bounds and the first group's row bounds are loaded
-  // BEFORE the dictionary staging, so their round trips overlap it instead
-  // of following its barrier
-  int32_t r0 = 0, r1 = 0, beg = 0, end = 0;
-  auto task_bounds = [&]() {
-    // both task bounds in one scalar load (K$), not a vector round trip
-    const int64_t tb = sload_i64(task_start, (uint64_t)t * 4u);
-    r0 = (int32_t)tb;
-    r1 = (int32_t)(tb >> 32);
-  };
-  auto first_end = [&]() { return align ? (r0 & ~(kWave - 1)) + kWave : r0 + kWave; };
-  const bool pre = XD && early;
-  PreChunk<T, U> pc;
-  if (pre && t < n_tasks) {
-    task_bounds();
-    if (r0 < r1) {
-      group_bounds(rp, r0, min(first_end(), r1), lane, beg, end);
-      if constexpr (XD && PF) {
-        // early = 2: the first chunk's positions / values too (the same
-        // loads wave_rows' stage_a issues for the run at the group's first
-        // row), so their HBM round trip runs under the staging
-        if (early == 2) {
-          const int32_t g1 = min(first_end(), r1);
-          const bool valid = r0 + lane < g1;
-          const unsigned long long skip = __ballot(valid && end - beg > long_t);
-          const int32_t b = skip ? r0 + (__ffsll(skip) - 1) : g1;
-          if (b > r0) {
-            const int32_t kb = __builtin_amdgcn_readfirstlane(__shfl(beg, 0, kWave));
-            const int32_t ke = __builtin_amdgcn_readfirstlane(__shfl(end, b - 1 - r0, kWave));
-            const int32_t n_run = ke - kb;
-            if (n_run > 0) {
-              const gchar *cb = uniform_ptr(cs.c16 + kb);
-              const gchar *vb = uniform_ptr(val + kb);
-              const int32_t last = min(kWave * U, n_run) - 1;
-#pragma unroll
-              for (int u = 0; u < U; ++u) {
-                const uint32_t j = (uint32_t)min(u * kWave + lane, last);
-                pc.col[u] = (int32_t)ld_off<NT, uint16_t>(cb, j * 2u);
-                pc.v[u] = ld_off<NT, T>(vb, j * (uint32_t)sizeof(T));
-              }
-              pc.valid = true;
-            }
-          }
-        }
-      }
-    }
-  }
-  // XD: the W packed tasks of the block share one staged dictionary
+  // XD: the W packed tasks of the block share one staged dictionary (loads
+  // of the task / row bounds and of the first chunk issued ahead of the
+  // staging measured -0.3 ... -0.6 % and cost 20 VGPRs: profiles/r05c,
+  // r05d; removed)
   if constexpr (XD) stage_xdict<T, W * 64>(reinterpret_cast<T *>(xdyn), x, xd, blk, threadIdx.x);
+  const int64_t t = blk * W + wid;
   if (t >= n_tasks) return;
 #if (HSPMV_DIAG & 8)
   const unsigned long long tb_stamp = diag_stamp();
 #endif
-  if (!pre) task_bounds();
+  // both task bounds in one scalar load (K$), not a vector round trip
+  const int64_t tb = sload_i64(task_start, (uint64_t)t * 4u);
+  const int32_t r0 = (int32_t)tb;
+  const int32_t r1 = (int32_t)(tb >> 32);
   if (r0 >= r1) return;
   T *my = lds + wid * wave_lds<U, false>();
   // group-base columns: one base per packed task
@@ -738,8 +678,9 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
 #endif
   // align: groups end on multiples of 64 rows (the SSR plan's aligned
   // pieces: every y store but an SSR's first and last covers whole lines)
-  const int32_t g1_first = min(first_end(), r1);
-  if (!pre) group_bounds(rp, r0, g1_first, lane, beg, end);
+  const int32_t g1_first = min(align ? (r0 & ~(kWave - 1)) + kWave : r0 + kWave, r1);
+  int32_t beg, end;
+  group_bounds(rp, r0, g1_first, lane, beg, end);
 #if (HSPMV_DIAG & 8)
   HSPMV_TRACE(ts, 1, diag_stamp());
 #endif
@@ -747,8 +688,7 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
     wave_rows<T, NT, U, PF, C16, XW, XD, HSPMV_COOP_GROUPS != 0>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
-                                         win, y_nt != 0, carry != 0, gbase, ts, &pc);
-    pc.valid = false;
+                                         win, y_nt != 0, carry != 0, gbase, ts);
     ts = nullptr;
     beg = nbeg;
     end = nend;
@@ -812,8 +752,8 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
 #define HSPMV_CSR3(W, C, XW, X)                                                               \
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C, W, XW, X>), dim3((unsigned)p.blocks),      \
                      dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,     \
-                     (int32_t)p.y_nt, p.carry, dp.task_align, p.early_bounds, dp.task_start, xw, xd,  \
-                     A.row_ptr, cs, val, x, y)
+                     (int32_t)p.y_nt, p.carry, dp.task_align, dp.task_start, xw, xd, A.row_ptr, cs, \
+                     val, x, y)
   if constexpr (XD) {  // packed tasks only (4 or 8 per block)
     if (p.waves_per_block == 8)
       HSPMV_CSR3(8, false, false, true);

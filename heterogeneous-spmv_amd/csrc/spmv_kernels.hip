@@ -382,10 +382,6 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   // r02r_ab_pf.jsonl)
   if (!p.prefetch && dtype == 1 && p.kernel == kCsr3 && A.has_xdict_tasks && !forced_u)
     p.prefetch = true;
-  // (bounds loaded ahead of the dictionary staging: C3 111.7 -> 111.0 us,
-  // fp32 65.4 -> 64.4, c3h flat -- under the 2 % a change must earn;
-  // profiles/r05c/ab_early_bounds.jsonl; A/B knob only)
-  p.early_bounds = t.early_bounds > 0 ? (t.early_bounds >= 2 ? 2 : 1) : 0;
   // Bank-padded product buffers (STREAM, no prefetch): when
   // the typical serially summed row is a multiple of 16 LDS words long
   // (fp32 rows of 16 / 32, fp64 rows of 8 / 16 / 24 / 32 ...), the lanes
