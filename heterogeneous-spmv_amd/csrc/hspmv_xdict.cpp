@@ -189,10 +189,9 @@ int64_t xd_target_entries(int dtype, const Tuning &t) {
   const int bpc = t.xd_blocks_per_cu > 0 ? t.xd_blocks_per_cu : kXdBlocksPerCu;
   const int64_t sv = (int64_t)dtype_size(dtype);
   // product staging of the chunk plan_launch picks for >= 12 nonzeros per
-  // row (pick_u: U = 4 fp64, 16 fp32), 4 waves, each 64 U values plus the
-  // bank padding of spmv_device.cuh lds_ix (one per 32: 2 U)
-  const int64_t u = sv == 8 ? 4 : 16;
-  const int64_t staging = 4 * (64 * u + 2 * u) * sv + 16;
+  // row (pick_u: U = 4 fp64, 16 fp32), 4 waves (CSR3 product buffers are
+  // never bank-padded: spmv_device.cuh wave_lds<U, false>)
+  const int64_t staging = 4 * 64 * (sv == 8 ? 4 : 16) * sv + 16;
   const int64_t per_block = (kLdsPerCu / bpc) / kLdsGranule * kLdsGranule;
   return std::max<int64_t>(0, (per_block - staging) / sv);
 }
