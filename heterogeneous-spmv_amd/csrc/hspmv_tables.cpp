@@ -243,7 +243,28 @@ void ssr_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> &o,
 // kernel's groups end on multiples of 64: DevPlan.task_align).  With more
 // pieces than waves, the adjacent pair with the fewest nonzeros merges until
 // W remain; with fewer, the last waves get empty tasks.
-bool ssr_aligned(const Tuning &t) { return t.csr3_plan == HSPMV_CSR3_PLAN_SSR && t.ssr_align > 0; }
+bool ssr_aligned(const Tuning &t) { return t.csr3_plan == HSPMV_CSR3_PLAN_SSR && t.ssr_align == 1; }
+
+// ssr_align = 2 (A/B): the SSR's rows split W ways by nonzeros at ROW
+// granularity (wave w starts at the first row reaching w/W of the SSR's
+// nonzeros), so the waves of a workgroup carry equal work whatever the
+// super-rows' sizes; a wave may run more than 64 rows (several groups).
+void ssr_tasks_rows(const int32_t *rp, int64_t m, const std::vector<int32_t> &o,
+                    const std::vector<int32_t> &in, int W, std::vector<int32_t> &ts) {
+  const int64_t nssr = (int64_t)o.size() - 1;
+  ts.assign((size_t)(nssr * W + 1), 0);
+  for (int64_t b = 0; b < nssr; ++b) {
+    const int32_t R0 = in[(size_t)o[(size_t)b]], R1 = in[(size_t)o[(size_t)b + 1]];
+    const int64_t k0 = rp[R0], k1 = rp[R1];
+    int32_t r = R0;
+    for (int w = 0; w < W; ++w) {
+      const int64_t target = k0 + (k1 - k0) * w / W;
+      while (r < R1 && rp[r] < target) ++r;
+      ts[(size_t)(b * W + w)] = w == 0 ? R0 : r;
+    }
+  }
+  ts[(size_t)(nssr * W)] = (int32_t)m;
+}
 
 void ssr_tasks_aligned(const int32_t *rp, int64_t m, const std::vector<int32_t> &o,
                        const std::vector<int32_t> &in, int W, std::vector<int32_t> &ts) {
@@ -359,6 +380,8 @@ void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner
     *waves = ssr_waves((double)m / (double)(outer->size() - 1));
     if (ssr_aligned(tune))
       ssr_tasks_aligned(rp, m, *outer, *inner, *waves, ts);
+    else if (tune.csr3_plan == HSPMV_CSR3_PLAN_SSR && tune.ssr_align == 2)
+      ssr_tasks_rows(rp, m, *outer, *inner, *waves, ts);
     else
       ssr_tasks(rp, m, *outer, *inner, *waves, ts);
     return;
