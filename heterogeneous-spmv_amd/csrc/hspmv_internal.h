@@ -59,7 +59,7 @@ struct Tuning {
   int stream_waves = 0;     // 0 auto, 1/2/4
   int deterministic = 0;    // 1: only kernels whose y bits never depend on scheduling
   int placement_trials = 0; // 0/1 off, K <= 8 array sets
-  int ssr_align = -1;       // SSR plan: waves take 64-row aligned pieces of their SSR (-1: default)
+  int ssr_align = -1;       // SSR plan wave cut: 2 row-granular nnz balance (-1: default), 0 super-rows, 1 aligned pieces
   // A/B only (diagnostic builds)
   int contig = 0;           // hipDeviceMallocContiguous allocations
   int xd_waves = 0;         // packed CSR3 tasks per dictionary block (0: 4; 8)

@@ -245,10 +245,19 @@ void ssr_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> &o,
 // W remain; with fewer, the last waves get empty tasks.
 bool ssr_aligned(const Tuning &t) { return t.csr3_plan == HSPMV_CSR3_PLAN_SSR && t.ssr_align == 1; }
 
-// ssr_align = 2 (A/B): the SSR's rows split W ways by nonzeros at ROW
-// granularity (wave w starts at the first row reaching w/W of the SSR's
-// nonzeros), so the waves of a workgroup carry equal work whatever the
-// super-rows' sizes; a wave may run more than 64 rows (several groups).
+// The SSR plan's wave cut (Tuning.ssr_align): 2 (default) row-granular
+// nonzero balance, 0 the super-row-granular cut (ssr_tasks), 1 aligned
+// pieces (ssr_tasks_aligned).
+int ssr_cut(const Tuning &t) { return t.ssr_align < 0 ? 2 : t.ssr_align; }
+
+// ssr_align = 2, the default since r05: the SSR's rows split W ways by
+// nonzeros at ROW granularity (wave w starts at the first row reaching w/W
+// of the SSR's nonzeros), so the waves of a workgroup carry equal work
+// whatever the super-rows' sizes -- the workgroup's LDS is held until its
+// slowest wave ends; a wave may run more than 64 rows (several groups).
+// One process (profiles/r05u/ab_ssr_rows.jsonl): C3 120.7 -> 118.2 us,
+// the MI355X grouping (64, 4) 126.6 -> 121.3, fp32 71.8 -> 71.5.  (r01's
+// row-granular cut capped waves at 64 rows and lost 7-30 % to long tails.)
 void ssr_tasks_rows(const int32_t *rp, int64_t m, const std::vector<int32_t> &o,
                     const std::vector<int32_t> &in, int W, std::vector<int32_t> &ts) {
   const int64_t nssr = (int64_t)o.size() - 1;
@@ -380,7 +389,7 @@ void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner
     *waves = ssr_waves((double)m / (double)(outer->size() - 1));
     if (ssr_aligned(tune))
       ssr_tasks_aligned(rp, m, *outer, *inner, *waves, ts);
-    else if (tune.csr3_plan == HSPMV_CSR3_PLAN_SSR && tune.ssr_align == 2)
+    else if (ssr_cut(tune) == 2)
       ssr_tasks_rows(rp, m, *outer, *inner, *waves, ts);
     else
       ssr_tasks(rp, m, *outer, *inner, *waves, ts);
