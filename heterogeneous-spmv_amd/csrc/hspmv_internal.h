@@ -59,6 +59,7 @@ struct Tuning {
   int stream_waves = 0;     // 0 auto, 1/2/4
   int deterministic = 0;    // 1: only kernels whose y bits never depend on scheduling
   int placement_trials = 0; // 0/1 off, K <= 8 array sets
+  int ssr_w = 0;            // SSR plan waves per workgroup (0: ssr_waves(); A/B)
   int ssr_align = -1;       // SSR plan wave cut: 2 row-granular nnz balance (-1: default), 0 super-rows, 1 aligned pieces
   // A/B only (diagnostic builds)
   int contig = 0;           // hipDeviceMallocContiguous allocations

@@ -89,6 +89,7 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_STREAM_W", &t->stream_waves);
   geti("HSPMV_PLACEMENT", &t->placement_trials);
   geti("HSPMV_SSR_ALIGN", &t->ssr_align);
+  geti("HSPMV_SSR_W", &t->ssr_w);
   geti("HSPMV_CONTIG", &t->contig);
   geti("HSPMV_XD_WAVES", &t->xd_waves);
   geti("HSPMV_XD_BPC", &t->xd_blocks_per_cu);

@@ -386,7 +386,9 @@ void build_tasks(const int32_t *rp, int64_t m, const std::vector<int32_t> *inner
   *waves = 4;
   if (!csr3_packed(tune)) {
     if (!inner || !outer || outer->size() < 2) return;
-    *waves = ssr_waves((double)m / (double)(outer->size() - 1));
+    *waves = (tune.ssr_w == 1 || tune.ssr_w == 2 || tune.ssr_w == 4 || tune.ssr_w == 8)
+                 ? tune.ssr_w  // A/B knob (diagnostic builds)
+                 : ssr_waves((double)m / (double)(outer->size() - 1));
     if (ssr_aligned(tune))
       ssr_tasks_aligned(rp, m, *outer, *inner, *waves, ts);
     else if (ssr_cut(tune) == 2)
