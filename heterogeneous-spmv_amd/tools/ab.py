@@ -91,11 +91,20 @@ def main():
                 t = _lib.Timing()
                 assert L.hspmv_run(h, 3, a.iters, C.byref(t)) == 0
                 times[i].append((t.t_min, t.t_avg))
+        # y again after the timed launches (racy paths: csort's atomic order,
+        # chunk stealing): largest |y - y_first| relative to |y_first| + 1e-30
+        rel = []
+        for L, h in zip(libs, hs):
+            y = np.empty(A.m, dtype=A.val.dtype)
+            assert L.hspmv_get_y(h, y.ctypes.data) == 0
+            d = np.abs(y.astype(np.float64) - ys[0].astype(np.float64))
+            rel.append(float((d / (np.abs(ys[0].astype(np.float64)) + 1e-30)).max()) if A.m else 0.0)
         for i, (L, h) in enumerate(zip(libs, hs)):
             rec = {"config": cfg, "lib": names[i], "kernel": a.kernel,
                    "t_min_us": round(min(t[0] for t in times[i]) * 1e6, 3),
                    "t_med_us": round(float(np.median([t[1] for t in times[i]])) * 1e6, 3),
-                   "y_equal_to_first": same[i], "placement_us": places[i]}
+                   "y_equal_to_first": same[i], "max_rel_vs_first_after": rel[i],
+                   "placement_us": places[i]}
             out.append(rec)
             print(json.dumps(rec), flush=True)
         for L, h in zip(libs, hs):
