@@ -114,7 +114,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
       const double target = tot * h / H;
       while (c < n && acc + (double)colcnt[(size_t)c] + wcol <= target) acc += (double)colcnt[(size_t)c++] + wcol;
       const int64_t eq = (n * h + H - 1) / H;
-      const int64_t slack = (int64_t)((kPartSlack - 1.0) * (double)(n / H));
+      const double ps = tn.csort_slack > 1.0 ? tn.csort_slack : kPartSlack;  // A/B knob
+      const int64_t slack = (int64_t)((ps - 1.0) * (double)(n / H));
       const int64_t lo = std::max(pb[(size_t)h - 1] + 1, eq - slack), hi = std::max(lo, eq + slack);
       pb[(size_t)h] = std::min(std::max(c, lo), hi);
     }

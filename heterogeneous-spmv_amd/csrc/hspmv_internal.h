@@ -79,6 +79,7 @@ struct Tuning {
   int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4)
   int csort_dyn = -1;                    // chunks claimed from an LDS queue (-1: the library's choice)
   double csort_sweep_w = 0;              // column-part cost of a column per row block (0: kSweepPerRowBlock)
+  double csort_slack = 0;                // widest column part / (n / H) when balancing (0: kPartSlack)
   int lds_pad = -1;                      // STREAM padded product buffers (-1: by row length, 0 off, 1 on)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
