@@ -22,8 +22,11 @@
 //   y.agent   : a relaxed atomic store at agent scope
 //   y.reg G=k : each wave keeps its k segments' sums in registers and stores
 //               them after the last one (no store between a wave's loads)
-//   y.defer   : persistent grid (256 CUs x 8 blocks), each block keeps its
+//   y.defer   : persistent grid (256 CUs x 4 blocks), each block keeps its
 //               rows' y in LDS and stores them all after its last segment
+//   regp (mode 3): persistent grid of 1024-4096 blocks (what the CUs hold
+//               at once), block b takes segments b, b + grid, ..., keeps the
+//               sums in registers, stores y after its last segment
 // Reported: ms (min of 10) and effective GB/s over the stream + y bytes.
 //
 //   hipcc -O3 --offload-arch=gfx950 bw_probe6.hip -o bw_probe6 && ./bw_probe6 [PER]
@@ -304,6 +307,41 @@ __global__ __launch_bounds__(256) void probe_defer(const uint16_t *__restrict__ 
     if (b * 256 + threadIdx.x < m) y[b * 256 + threadIdx.x] = ys[k * 256 + threadIdx.x];
 }
 
+// persistent at full occupancy: the grid is what the CUs hold at once
+// (gridDim.x blocks), block b takes segments b, b + G, ... (at most K, so
+// the blocks in flight read neighbouring rows), keeps each segment's sums
+// in registers and stores them all after its last segment (YS = 0: no y)
+template <int K, bool YS>
+__global__ __launch_bounds__(256) void probe_regp(const uint16_t *__restrict__ pos,
+                                                  const double *__restrict__ val,
+                                                  double *__restrict__ y, long m, int per,
+                                                  double *__restrict__ out) {
+  __shared__ double lds[4 * 64 * U];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long nnz = m * per;
+  const long nseg = (m + 255) / 256;
+  double keep[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const long b = blockIdx.x + (long)k * gridDim.x;
+    keep[k] = 0.0;
+    if (b < nseg) {
+      const long w = b * 4 + wid;
+      const long s0 = std::min(w * 64 * per, nnz), s1 = std::min(s0 + 64L * per, nnz);
+      keep[k] = segment(pos, val, s0, s1, lane, lds + wid * 64 * U);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const long r = (blockIdx.x + (long)k * gridDim.x) * 256 + threadIdx.x;
+    if constexpr (YS) {
+      if (r < m) y[r] = keep[k];
+    } else {
+      if (keep[k] == 12345.678) out[0] = keep[k];
+    }
+  }
+}
+
 template <typename F>
 float time_ms(F launch, int reps) {
   hipEvent_t a, b;
@@ -348,6 +386,34 @@ int main(int argc, char **argv) {
     const float ms = time_ms([&] { hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, 0, pos, val, y, m, per, out); }, 10);
     report(name, ms, bytes);
   };
+  if (argc > 3 && atoi(argv[3]) == 3) {  // persistent register-deferred y vs the plain grid
+    auto runp = [&](auto kern, const char *name, double bytes, unsigned g) {
+      const float ms = time_ms([&] { hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, 0, pos, val, y, m, per, out); }, 10);
+      report(name, ms, bytes);
+    };
+    const long nseg = (m + 255) / 256;
+    for (int rep = 0; rep < 2; ++rep) {
+      run(probe<Y_NONE>, "base", sb);
+      run(probe<Y_WAVE>, "y.wave", sb + yb);
+      if (nseg <= 8L * 2048) {
+        runp(probe_regp<8, false>, "regp base 1024 blocks", sb, 1024);
+        runp(probe_regp<8, true>, "regp y 1024 blocks", sb + yb, 1024);
+      }
+      if (nseg <= 4L * 2048) {
+        runp(probe_regp<4, false>, "regp base 2048 blocks", sb, 2048);
+        runp(probe_regp<4, true>, "regp y 2048 blocks", sb + yb, 2048);
+      }
+      if (nseg <= 6L * 1280) {
+        runp(probe_regp<6, false>, "regp base 1280 blocks", sb, 1280);
+        runp(probe_regp<6, true>, "regp y 1280 blocks", sb + yb, 1280);
+      }
+      if (nseg <= 2L * 4096) {
+        runp(probe_regp<2, false>, "regp base 4096 blocks", sb, 4096);
+        runp(probe_regp<2, true>, "regp y 4096 blocks", sb + yb, 4096);
+      }
+    }
+    return 0;
+  }
   const bool reg_only = argc > 3 && atoi(argv[3]) == 1;
   if (argc > 3 && atoi(argv[3]) == 2) {
     for (int rep = 0; rep < 2; ++rep) {
