@@ -7,8 +7,9 @@ clustered columns, sorted or unsorted columns with duplicates, exact zeros,
 m and n from 1 up, fp32 or fp64.  Every case runs AUTO, STREAM, VECTOR (a
 random lane count), CSR3 with freshly built maps under the aligned / packed /
 ssr plans, csort (auto and 4 column parts), AUTO with deterministic = 1,
-STREAM with split rows kept whole, and AUTO over 2 x slabs, each twice (two x
-vectors through one handle: no state may leak from one launch into the next).
+STREAM with split rows kept whole, AUTO over 2 x slabs, and AUTO over three
+row-range shards, each twice (two x vectors through one handle: no state may
+leak from one launch into the next).
 
 Bars (spmv-csr/spmv.c:92-114 restated by the oracle):
 * fp64: |y - y64| <= 1e-6 |y64| + 1e-12 sum|a x| (north star);
@@ -93,6 +94,7 @@ def runs(A, rng):
     yield "auto-det", {"options": {"deterministic": 1}}
     yield "stream-whole-rows", {"kernel": "stream", "split_rows": False}
     yield "auto-2slabs", {"options": {"x_slabs": 2}}
+    yield "sharded-3", {"devices": [0, 0, 0]}  # row-range shards (one device, repeated)
 
 
 def check(A, x, y, ordered, what):
@@ -130,7 +132,7 @@ def test_fuzz_every_kernel_matches_oracle(seed):
                 check(A, x, y, name in ("stream", "csr3"), (desc, label, name, i))
         ran.append((label, name))
         SEEN.add(name)
-    assert len(ran) >= 9, (desc, ran)
+    assert len(ran) >= 10, (desc, ran)
 
 
 def test_fuzz_ran_every_kernel():
