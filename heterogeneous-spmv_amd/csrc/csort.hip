@@ -162,13 +162,13 @@ __device__ __forceinline__ void load_entries(const void *__restrict__ ent, const
 
 // S: the LDS row-slot / partial-sum type (double; float only for fp32 data,
 // an A/B variant with half the LDS per row).
-template <typename T, typename S, int U, bool NT, bool PF, bool WIDE>
+template <typename T, typename S, typename P, int U, bool NT, bool PF, bool WIDE>
 __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     int32_t H, int64_t m, int32_t direct, const int32_t *__restrict__ blk_c,
     const int32_t *__restrict__ blk_r, const int32_t *__restrict__ blk_v,
     const int32_t *__restrict__ vslice, const int32_t *__restrict__ cbase,
     const void *__restrict__ ent, const T *__restrict__ val, const T *__restrict__ x,
-    S *__restrict__ part, S *__restrict__ spart, T *__restrict__ y,
+    P *__restrict__ part, S *__restrict__ spart, T *__restrict__ y,
     unsigned long long *__restrict__ trace, int32_t dyn) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int32_t next_chunk;  // dyn: the workgroup's chunk queue head
@@ -305,8 +305,8 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) y[r0 + i] = (T)acc[i];
     return;
   }
-  S *out = part + (int64_t)h * m + r0;
-  for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) out[i] = acc[i];
+  P *out = part + (int64_t)h * m + r0;
+  for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) out[i] = (P)acc[i];
   for (int32_t i = threadIdx.x; i < nv; i += kCsortThreads) spart[vslice[v0 + i]] = acc[nr + i];
 }
 
@@ -315,22 +315,26 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
 // fixed lane assignment and shuffle tree).
 // R rows per thread (1, 2, 4): R-element partial loads (16 / 32 bytes for
 // R = 2 / 4; m a multiple of R keeps every part's rows aligned).
-template <typename T, typename S, int R>
+template <typename T, typename S, typename P, int R>
 __global__ __launch_bounds__(256) void hspmv_csort_finish(
-    int64_t m, int32_t H, int64_t row_blocks, const S *__restrict__ part,
+    int64_t m, int32_t H, int64_t row_blocks, const P *__restrict__ part,
     const uint32_t *__restrict__ long_mask, int32_t n_long, const int32_t *__restrict__ long_row,
     const int32_t *__restrict__ long_cs, const S *__restrict__ spart, T *__restrict__ y) {
   if ((int64_t)blockIdx.x < row_blocks) {
     if constexpr (R > 1) {
       typedef S sr __attribute__((ext_vector_type(R)));
+      typedef P pr __attribute__((ext_vector_type(R)));
       typedef T tr __attribute__((ext_vector_type(R)));
       const int64_t r = R * ((int64_t)blockIdx.x * 256 + threadIdx.x);
       if (r >= m) return;
-      sr s = *reinterpret_cast<const sr *>(part + r);
-      for (int32_t h = 1; h < H; ++h) {
-        const sr q = *reinterpret_cast<const sr *>(part + (int64_t)h * m + r);
+      const pr p0 = *reinterpret_cast<const pr *>(part + r);
+      sr s;
 #pragma unroll
-        for (int j = 0; j < R; ++j) s[j] += q[j];
+      for (int j = 0; j < R; ++j) s[j] = (S)p0[j];
+      for (int32_t h = 1; h < H; ++h) {
+        const pr q = *reinterpret_cast<const pr *>(part + (int64_t)h * m + r);
+#pragma unroll
+        for (int j = 0; j < R; ++j) s[j] += (S)q[j];
       }
       // R <= 4 rows never straddle a 32-row mask word (r is a multiple of R)
       const uint32_t lm = long_mask ? (long_mask[r >> 5] >> (r & 31)) & ((1u << R) - 1u) : 0u;
@@ -349,8 +353,8 @@ __global__ __launch_bounds__(256) void hspmv_csort_finish(
       const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
       if (r >= m) return;
       if (long_mask && ((long_mask[r >> 5] >> (r & 31)) & 1u)) return;
-      S s = part[r];
-      for (int32_t h = 1; h < H; ++h) s += part[(int64_t)h * m + r];
+      S s = (S)part[r];
+      for (int32_t h = 1; h < H; ++h) s += (S)part[(int64_t)h * m + r];
       y[r] = (T)s;
       return;
     }
@@ -365,36 +369,37 @@ __global__ __launch_bounds__(256) void hspmv_csort_finish(
   if (lane == 0) y[long_row[j]] = (T)s;
 }
 
-template <typename T, typename S, int R>
-void launch_finish(const DevCsort &c, const S *part, const S *spart, T *y, hipStream_t st) {
+template <typename T, typename S, typename P, int R>
+void launch_finish(const DevCsort &c, const P *part, const S *spart, T *y, hipStream_t st) {
   const int64_t lb = ((int64_t)c.n_long + 3) / 4;
   const int64_t rb = (c.m / R + 255) / 256;
-  hipLaunchKernelGGL((hspmv_csort_finish<T, S, R>), dim3((unsigned)(rb + lb)), dim3(256), 0, st, c.m, c.H,
+  hipLaunchKernelGGL((hspmv_csort_finish<T, S, P, R>), dim3((unsigned)(rb + lb)), dim3(256), 0, st, c.m, c.H,
                      rb, part, c.long_mask, c.n_long, c.long_row, c.long_cs, spart, y);
 }
 
-template <typename T, typename S, int U, bool NT, bool PF, bool WIDE>
-void launch_csort_main(const DevCsort &c, const T *x, S *part, S *spart, T *y, hipStream_t st) {
-  hipLaunchKernelGGL((hspmv_csort<T, S, U, NT, PF, WIDE>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
+template <typename T, typename S, typename P, int U, bool NT, bool PF, bool WIDE>
+void launch_csort_main(const DevCsort &c, const T *x, P *part, S *spart, T *y, hipStream_t st) {
+  hipLaunchKernelGGL((hspmv_csort<T, S, P, U, NT, PF, WIDE>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
                      (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
                      c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y,
                      c.trace, c.dyn ? 1 : 0);
 }
 
-template <typename T, typename S, int U, bool NT>
-hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
-  S *part = static_cast<S *>(c.part), *spart = static_cast<S *>(c.spart);
+template <typename T, typename S, typename P, int U, bool NT>
+hipError_t launch_csort_p(const DevCsort &c, const T *x, T *y, hipStream_t st) {
+  P *part = static_cast<P *>(c.part);
+  S *spart = static_cast<S *>(c.spart);
   if constexpr (sizeof(T) == 8 && U % 4 != 0) {
     if (c.wide) return hipErrorInvalidValue;
-    if (c.prefetch) launch_csort_main<T, S, U, NT, true, false>(c, x, part, spart, y, st);
-    else launch_csort_main<T, S, U, NT, false, false>(c, x, part, spart, y, st);
+    if (c.prefetch) launch_csort_main<T, S, P, U, NT, true, false>(c, x, part, spart, y, st);
+    else launch_csort_main<T, S, P, U, NT, false, false>(c, x, part, spart, y, st);
   } else {
     if (c.prefetch) {
-      if (c.wide) launch_csort_main<T, S, U, NT, true, true>(c, x, part, spart, y, st);
-      else launch_csort_main<T, S, U, NT, true, false>(c, x, part, spart, y, st);
+      if (c.wide) launch_csort_main<T, S, P, U, NT, true, true>(c, x, part, spart, y, st);
+      else launch_csort_main<T, S, P, U, NT, true, false>(c, x, part, spart, y, st);
     } else {
-      if (c.wide) launch_csort_main<T, S, U, NT, false, true>(c, x, part, spart, y, st);
-      else launch_csort_main<T, S, U, NT, false, false>(c, x, part, spart, y, st);
+      if (c.wide) launch_csort_main<T, S, P, U, NT, false, true>(c, x, part, spart, y, st);
+      else launch_csort_main<T, S, P, U, NT, false, false>(c, x, part, spart, y, st);
     }
   }
   hipError_t e = hipGetLastError();
@@ -407,12 +412,21 @@ hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
   const int fr = c.fin_rows > 0 ? c.fin_rows : 4;
   const uintptr_t ya = reinterpret_cast<uintptr_t>(y);
   if (fr >= 4 && c.m % 4 == 0 && ya % (4 * sizeof(T)) == 0)
-    launch_finish<T, S, 4>(c, part, spart, y, st);
+    launch_finish<T, S, P, 4>(c, part, spart, y, st);
   else if (fr >= 2 && c.m % 2 == 0 && ya % (2 * sizeof(T)) == 0)
-    launch_finish<T, S, 2>(c, part, spart, y, st);
+    launch_finish<T, S, P, 2>(c, part, spart, y, st);
   else
-    launch_finish<T, S, 1>(c, part, spart, y, st);
+    launch_finish<T, S, P, 1>(c, part, spart, y, st);
   return hipGetLastError();
+}
+
+// part32 (A/B, fp32 data over fp64 slots only): the column parts' row
+// partials stored as fp32 (half the partial traffic; y then rounds twice)
+template <typename T, typename S, int U, bool NT>
+hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
+  if constexpr (sizeof(T) == 4 && sizeof(S) == 8)
+    if (c.part32) return launch_csort_p<T, S, float, U, NT>(c, x, y, st);
+  return launch_csort_p<T, S, S, U, NT>(c, x, y, st);
 }
 
 template <typename T, typename S, bool NT>

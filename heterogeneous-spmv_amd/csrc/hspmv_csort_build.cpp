@@ -517,7 +517,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   }
   const bool direct = H == 1 && lrow.empty();
   if (!direct) {  // partial sums in the slot type
-    if ((rc = dev_alloc(&s.d_cs_part, slot_bytes * (size_t)H * (size_t)m, &s.bytes))) return rc;
+    const int64_t part_bytes = (dtype == HSPMV_F32 && !slot32 && tn.csort_part32 == 1) ? 4 : slot_bytes;
+    if ((rc = dev_alloc(&s.d_cs_part, part_bytes * (size_t)H * (size_t)m, &s.bytes))) return rc;
     if ((rc = dev_alloc(&s.d_cs_spart, slot_bytes * (size_t)std::max<int64_t>(n_slices, 1), &s.bytes)))
       return rc;
   }
@@ -540,6 +541,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.prefetch = wide && dtype == HSPMV_F32;  // see `wide` above
   if (tn.csort_pf >= 0) c.prefetch = tn.csort_pf != 0;
   c.slot32 = slot32;
+  c.part32 = dtype == HSPMV_F32 && !slot32 && tn.csort_part32 == 1;
   c.wide = wide;
   c.fin_rows = tn.csort_fin_rows;
   // waves claim chunks from the workgroup's LDS queue: one process, 7

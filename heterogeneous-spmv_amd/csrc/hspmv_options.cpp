@@ -86,6 +86,7 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_CSORT_DYN", &t->csort_dyn);
   if (const char *e = getenv("HSPMV_CSORT_SWEEP")) t->csort_sweep_w = atof(e);
   if (const char *e = getenv("HSPMV_CSORT_SLACK")) t->csort_slack = atof(e);
+  geti("HSPMV_CSORT_PART32", &t->csort_part32);
   geti("HSPMV_LDS_PAD", &t->lds_pad);
   geti("HSPMV_STREAM_W", &t->stream_waves);
   geti("HSPMV_PLACEMENT", &t->placement_trials);
