@@ -516,8 +516,9 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     s.d_cs_val = dv;
   }
   const bool direct = H == 1 && lrow.empty();
-  if (!direct) {  // partial sums in the slot type
-    const int64_t part_bytes = (dtype == HSPMV_F32 && !slot32 && tn.csort_part32 == 1) ? 4 : slot_bytes;
+  // row partials in the slot type (fp32 with the part32 A/B knob)
+  const int64_t part_bytes = (dtype == HSPMV_F32 && !slot32 && tn.csort_part32 == 1) ? 4 : slot_bytes;
+  if (!direct) {
     if ((rc = dev_alloc(&s.d_cs_part, part_bytes * (size_t)H * (size_t)m, &s.bytes))) return rc;
     if ((rc = dev_alloc(&s.d_cs_spart, slot_bytes * (size_t)std::max<int64_t>(n_slices, 1), &s.bytes)))
       return rc;
@@ -578,7 +579,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   // partial sums written and read back + y
   const double xb = (double)s.x_entries * (double)sv;
   const double part_traffic =
-      direct ? 0.0 : 2.0 * (double)slot_bytes * ((double)H * (double)m + (double)n_slices);
+      direct ? 0.0
+             : 2.0 * ((double)part_bytes * (double)H * (double)m + (double)slot_bytes * (double)n_slices);
   s.csort_format_bytes = (double)tot * (double)(4 + sv) + 4.0 * (double)tot_chunks + xb + part_traffic +
                          (double)sv * (double)m;
   s.A.has_csort = true;
