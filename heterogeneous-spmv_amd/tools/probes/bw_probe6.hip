@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void probe_defer(const uint16_t *__restrict__ 
 // (gridDim.x blocks), block b takes segments b, b + G, ... (at most K, so
 // the blocks in flight read neighbouring rows), keeps each segment's sums
 // in registers and stores them all after its last segment (YS = 0: no y)
-template <int K, bool YS>
+template <int K, bool YS, int YM = 0>
 __global__ __launch_bounds__(256) void probe_regp(const uint16_t *__restrict__ pos,
                                                   const double *__restrict__ val,
                                                   double *__restrict__ y, long m, int per,
@@ -334,8 +334,12 @@ __global__ __launch_bounds__(256) void probe_regp(const uint16_t *__restrict__ p
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const long r = (blockIdx.x + (long)k * gridDim.x) * 256 + threadIdx.x;
-    if constexpr (YS) {
+    if constexpr (YS && YM == 0) {
       if (r < m) y[r] = keep[k];
+    } else if constexpr (YS && YM == 1) {  // into a 1 MiB window (stays in L2)
+      if (r < m) y[r & 0x1FFFF] = keep[k];
+    } else if constexpr (YS && YM == 2) {  // one lane per wave (8 B)
+      if (lane == 0 && r < m) y[r] = keep[k];
     } else {
       if (keep[k] == 12345.678) out[0] = keep[k];
     }
@@ -402,6 +406,12 @@ int main(int argc, char **argv) {
       if (nseg <= 4L * 2048) {
         runp(probe_regp<4, false>, "regp base 2048 blocks", sb, 2048);
         runp(probe_regp<4, true>, "regp y 2048 blocks", sb + yb, 2048);
+        runp(probe_regp<4, true, 1>, "regp y.l2 2048 blocks", sb + yb, 2048);
+        runp(probe_regp<4, true, 2>, "regp y.lane0 2048 blocks", sb + yb, 2048);
+      }
+      if (nseg <= 8L * 1024) {
+        runp(probe_regp<8, true, 1>, "regp y.l2 1024 blocks", sb + yb, 1024);
+        runp(probe_regp<8, true, 2>, "regp y.lane0 1024 blocks", sb + yb, 1024);
       }
       if (nseg <= 6L * 1280) {
         runp(probe_regp<6, false>, "regp base 1280 blocks", sb, 1280);
