@@ -442,10 +442,20 @@ static int fill_info(hspmv_handle *h, hspmv_info *out) {
 
 extern "C" {
 
+// The 1.0 layout only (HSPMV_INFO_SIZE_1_0 bytes, frozen for major 1): a
+// 1.0 caller's struct is that large whatever this library's hspmv_info is.
+static_assert(sizeof(hspmv_info) >= HSPMV_INFO_SIZE_1_0, "hspmv_info shrank below its 1.0 layout");
+static_assert(offsetof(hspmv_info, heavy_group_frac) + sizeof(double) == HSPMV_INFO_SIZE_1_0,
+              "HSPMV_INFO_SIZE_1_0 must end at the last 1.0 field");
+
 int hspmv_get_info(hspmv_handle *h, hspmv_info *out) {
   clear_error();
   if (!out) return set_error(HSPMV_E_INVALID, "NULL output");
-  return fill_info(h, out);
+  hspmv_info full;
+  const int rc = fill_info(h, &full);
+  if (rc) return rc;
+  memcpy(out, &full, HSPMV_INFO_SIZE_1_0);
+  return HSPMV_OK;
 }
 
 #ifdef HSPMV_ENV_KNOBS

@@ -19,6 +19,7 @@
 // The entry lines are parsed in parallel (split at line boundaries,
 // std::from_chars), then bucketed by row with a counting sort.
 #include <errno.h>
+#include <locale.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -61,12 +62,13 @@ bool parse_line(const char *p, const char *e, bool pattern, long long rows, long
     auto r = std::from_chars(p, e, v);
     if (r.ec == std::errc::result_out_of_range) {
       // from_chars leaves v unset here; strtod gives what mmread's fscanf
-      // gives: +-HUGE_VAL on overflow, a denormal or +-0 on underflow
-      char tok[128];
-      const size_t n = std::min<size_t>((size_t)(r.ptr - p), sizeof(tok) - 1);
-      memcpy(tok, p, n);
-      tok[n] = 0;
-      v = strtod(tok, nullptr);
+      // gives: +-HUGE_VAL on overflow, a denormal or +-0 on underflow.  The
+      // whole token (any length: a 400-digit literal must overflow, not be
+      // cut to 127 digits) in the C locale (a comma-decimal LC_NUMERIC must
+      // not stop the parse at the '.').
+      static const locale_t c_loc = newlocale(LC_ALL_MASK, "C", (locale_t)0);
+      const std::string tok(p, r.ptr);
+      v = strtod_l(tok.c_str(), nullptr, c_loc);
     } else if (r.ec != std::errc()) {
       return false;
     }

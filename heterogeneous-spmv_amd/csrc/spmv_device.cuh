@@ -718,11 +718,8 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
   hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C, XW, XDX, W, PAD>), dim3((unsigned)p.blocks), \
                      dim3(W * 64), dyn, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk, (int32_t)p.groups,  \
                      (int32_t)p.y_nt, p.carry, A.row_ptr, cs, xw, xd, val, x, y)
-    if constexpr (XD) {
-      if (p.lds_pad && !PF)
-        HSPMV_STREAM(false, false, true, 4, true);
-      else
-        HSPMV_STREAM(false, false, true, 4, false);
+    if constexpr (XD) {  // never padded (plan_launch: dictionaries are sized unpadded)
+      HSPMV_STREAM(false, false, true, 4, false);
       return;
     }
     // padded product buffers (LaunchPlan.lds_pad): conflicting row lengths,

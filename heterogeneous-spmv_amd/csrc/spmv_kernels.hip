@@ -388,16 +388,21 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
   // walking those rows hit at most two banks.  Dense 32x32 blocks: fp64
   // 129.6 -> 95.1 us, fp32 99.6 -> 67.1; fp64 rows of 24: 103.2 -> 95.9;
   // fp32 rows of 24 (8-word multiples) lose 3 % padded, so they are left
-  // alone (profiles/r05j/ab_lds_pad.jsonl).
-  {
-    const int words = A.serial_len * (dtype == 1 ? 2 : 1);
-    const bool conflicting = words > 0 && (words % 16) == 0;
-    p.lds_pad = p.kernel == kStream && !p.prefetch && conflicting;
-    if (t.lds_pad >= 0) p.lds_pad = p.kernel == kStream && !p.prefetch && t.lds_pad > 0;
-  }
+  // alone (profiles/r05j/ab_lds_pad.jsonl).  Decided after the A/B
+  // overrides, so that hspmv_info.lds_pad reports the launch that runs (the
+  // PF variant has no padded form).  Never with x dictionaries: those are
+  // sized (hspmv_xdict.cpp xd_target_entries) against unpadded product
+  // buffers, and the pad would cost the launch a workgroup per CU.
   if (t.pf >= 0) p.prefetch = t.pf != 0;  // A/B knobs (diagnostic builds only)
   if (t.y_nt >= 0) p.y_nt = t.y_nt != 0;
   if (t.nt >= 0) p.nontemporal = t.nt != 0;
+  {
+    const int words = A.serial_len * (dtype == 1 ? 2 : 1);
+    const bool conflicting = words > 0 && (words % 16) == 0;
+    const bool can_pad = p.kernel == kStream && !p.prefetch && !A.has_xdict;
+    p.lds_pad = can_pad && conflicting;
+    if (t.lds_pad >= 0) p.lds_pad = can_pad && t.lds_pad > 0;
+  }
   p.dyn_lds = t.dyn_lds;
   return p;
 }

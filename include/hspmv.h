@@ -378,8 +378,11 @@ int hspmv_get_y(hspmv_handle *h, void *y_host);
  * every GPU's full-length buffer, timed (seconds).  Either pointer may be NULL. */
 int hspmv_exchange(hspmv_handle *h, double *bcast_x_s, double *gather_y_s);
 
-/* Fills the whole hspmv_info of this major (1.x callers; NULL -> E_INVALID).
- * A caller built against an older 1.x header uses hspmv_get_info_sized. */
+/* Fills the 1.0 layout of hspmv_info -- exactly HSPMV_INFO_SIZE_1_0 bytes,
+ * in every 1.x library, so a 1.0 binary's stack struct is never overrun
+ * when a later minor grows hspmv_info (NULL -> E_INVALID).  Fields added
+ * after 1.0 come only from hspmv_get_info_sized. */
+#define HSPMV_INFO_SIZE_1_0 248
 int hspmv_get_info(hspmv_handle *h, hspmv_info *out);
 /* Fills min(out_size, sizeof(hspmv_info)) bytes: pass sizeof(hspmv_info) of
  * the header you were built against. */

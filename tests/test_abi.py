@@ -118,6 +118,44 @@ def test_abi_major_is_in_the_soname():
     assert "Shared library: [libhspmv.so.1]" in out.stdout
 
 
+def test_old_major_binary_does_not_resolve_the_library(tmp_path):
+    """A binary with NEEDED libhspmv.so (what linking against a 0.x library
+    gave) and the CLIs' search path (rpath = build/) finds no library: the
+    link-time symlink lives in build/dev/, off every runtime path, and
+    build/ holds only libhspmv.so.1."""
+    build = _lib.LIB_PATH.parent
+    assert not (build / "libhspmv.so").exists()
+    dev = build / "dev" / "libhspmv.so"
+    assert dev.is_symlink() and dev.resolve() == _lib.LIB_PATH.resolve()
+    # a stand-in 0.x library: no SONAME, so NEEDED records libhspmv.so
+    old = tmp_path / "old"
+    old.mkdir()
+    (tmp_path / "stub.c").write_text("int hspmv_version_stub(void) { return 0; }\n")
+    subprocess.run(["gcc", "-shared", "-fPIC", str(tmp_path / "stub.c"), "-o", str(old / "libhspmv.so")],
+                   check=True)
+    (tmp_path / "main.c").write_text("int hspmv_version_stub(void);\n"
+                                     "int main(void) { return hspmv_version_stub(); }\n")
+    exe = tmp_path / "old_cli"
+    subprocess.run(["gcc", str(tmp_path / "main.c"), "-o", str(exe), "-L", str(old), "-lhspmv",
+                    f"-Wl,-rpath,{build}", "-Wl,--disable-new-dtags"], check=True)
+    needed = subprocess.run(["readelf", "-d", str(exe)], capture_output=True, text=True).stdout
+    assert "Shared library: [libhspmv.so]" in needed
+    env = {k: v for k, v in __import__("os").environ.items() if k != "LD_LIBRARY_PATH"}
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env)
+    assert r.returncode != 0 and "libhspmv.so" in r.stderr
+
+
+def test_get_info_writes_the_frozen_1_0_layout():
+    """hspmv_get_info writes HSPMV_INFO_SIZE_1_0 bytes in every 1.x library
+    (a 1.0 binary's struct is that large); fields added later come only from
+    hspmv_get_info_sized.  The constant ends at the last 1.0 field."""
+    text = _lib.HEADER.read_text()
+    import re as _re
+    n = int(_re.search(r"#define HSPMV_INFO_SIZE_1_0 (\d+)", text).group(1))
+    assert n == _lib.Info.heavy_group_frac.offset + 8
+    assert ctypes.sizeof(_lib.Info) >= n
+
+
 def test_get_info_rejects_null_without_a_handle():
     """hspmv_get_info / hspmv_get_info_sized with NULL arguments return
     HSPMV_E_INVALID (no GPU: the handle-free paths only; the NULL-output
@@ -149,3 +187,10 @@ def test_get_info_null_output_and_canary():
         assert L.hspmv_get_info_sized(h, ctypes.cast(buf, ctypes.POINTER(_lib.Info)), n01) == 0
         assert all(buf[i] == 0xA5 for i in range(n01, len(buf)))
         assert bytes(buf[:n01]) == bytes(memoryview(full).cast("B")[:n01])
+        # hspmv_get_info: exactly the frozen 1.0 size, whatever sizeof(hspmv_info) is
+        n10 = _lib.Info.heavy_group_frac.offset + 8
+        for i in range(len(buf)):
+            buf[i] = 0xA5
+        assert L.hspmv_get_info(h, ctypes.cast(buf, ctypes.POINTER(_lib.Info))) == 0
+        assert all(buf[i] == 0xA5 for i in range(n10, len(buf)))
+        assert bytes(buf[:n10]) == bytes(memoryview(full).cast("B")[:n10])

@@ -128,6 +128,20 @@ def test_read_mtx_out_of_range_values(tmp_path):
     assert (2, 2) not in d and A.nnz == 3
 
 
+def test_read_mtx_long_overflowing_token(tmp_path):
+    """A 400-digit literal with no exponent overflows to +Inf (the whole
+    token is parsed, not its first 127 characters), and a tiny literal
+    written with 400 leading zeros underflows to a dropped zero."""
+    big = "9" * 400
+    tiny = "0." + "0" * 400 + "1"
+    f = tmp_path / "long.mtx"
+    f.write_text("%%MatrixMarket matrix coordinate real general\n2 2 3\n"
+                 f"1 1 {big}\n2 2 -{big}.5\n1 2 {tiny}\n")
+    A = hspmv.read_mtx(f, np.float64)
+    assert A.nnz == 2
+    assert A.val[0] == np.inf and A.val[1] == -np.inf
+
+
 def test_read_mtx_large_parallel(tmp_path):
     # enough lines that every parse thread gets a share, CRLF line ends
     A = gen.powerlaw(20000, seed=3, dtype=np.float64)
