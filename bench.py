@@ -27,7 +27,11 @@ Extra fields on the line:
   roofline     one SpMV (the kernel launch(es) of a step), algorithmic bytes
                per SpMV / HIP-event-timed average over the timed region on
                the launch stream, vs 8 TB/s HBM; traffic from the committed
-               rocprofv3 PMC summary for this workload (profiles/*_pmc.json)
+               rocprofv3 PMC summary for this workload (profiles/*_pmc.json).
+               Every leg runs inside a roctx range (bench:headline,
+               bench:headline_cold, bench:plan_packed, bench:plan_ssr,
+               bench:n1_<cfg>[_cold]): rocprofv3 --kernel-trace --marker-trace
+               --kernel-rename --stats then reports each leg's kernels apart
   cold         the same SpMV with the 256 MiB Infinity Cache evicted before
                every launch (a 512 MiB read)
   comm         RCCL x broadcast / y all-gather / halo-exchange times (N > 1),
@@ -144,6 +148,61 @@ def dry_run(args) -> None:
         out["plan"] = {"config": cfg, "world": args.gpus, "scaling": "strong",
                        "note": "row lengths known only after generating the matrix"}
     print(json.dumps(out), flush=True)
+
+
+# ------------------------------------------------------------------ trace ranges
+
+class _Roctx:
+    """roctx ranges around the bench's legs, so that a rocprofv3 run of this
+    script with ``--kernel-trace --marker-trace --kernel-rename --stats``
+    reports each leg's kernels under the leg's name (the headline's aligned
+    CSR-3 launches apart from the packed / ssr legs, which launch the same
+    kernel template).  Loaded from ROCm's roctx library through ctypes; a
+    no-op when it is absent.  Outside a profiler the calls cost nothing
+    measurable and sit outside every timed region."""
+
+    def __init__(self):
+        self.lib = None
+        self.tried = False  # loaded on first use: the self-launching parent never loads it
+
+    def load(self):
+        self.tried = True
+        import ctypes
+        for name in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"):
+            try:
+                self.lib = ctypes.CDLL(name)
+                self.lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                break
+            except OSError:
+                continue
+
+    def push(self, name: str) -> None:
+        if not self.tried:
+            self.load()
+        if self.lib is not None:
+            self.lib.roctxRangePushA(name.encode())
+
+    def pop(self) -> None:
+        if self.lib is not None:
+            self.lib.roctxRangePop()
+
+
+ROCTX = _Roctx()
+
+
+class leg_range:
+    """``with leg_range("bench:headline"): ...`` -- one roctx range."""
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        ROCTX.push(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        ROCTX.pop()
+        return False
 
 
 # ------------------------------------------------------------------ torch plumbing
@@ -305,23 +364,25 @@ def single_gpu_point(args, stream, cfg: str):
     steps = max(10, args.steps // 10)
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(steps):
-        op.spmv()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    step_s = (time.perf_counter() - t0) / steps
+    with leg_range(f"bench:n1_{cfg}"):
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(steps):
+            op.spmv()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        step_s = (time.perf_counter() - t0) / steps
     ev_s = ev0.elapsed_time(ev1) * 1e-3 / steps
     flush = torch.ones(64 << 20, dtype=torch.float64, device="cuda")
     cold = []
     for _ in range(max(3, args.cold_steps)):
         flush.sum()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        op.spmv()
-        b.record(stream)
-        torch.cuda.synchronize()
+        with leg_range(f"bench:n1_{cfg}_cold"):
+            a.record(stream)
+            op.spmv()
+            b.record(stream)
+            torch.cuda.synchronize()
         cold.append(a.elapsed_time(b) * 1e-3)
     del flush
     cold_s = float(np.median(cold))
@@ -390,11 +451,12 @@ def csr3_maps_plans(args, A, maps, x, y_ref, stream, device):
             op.spmv()
         torch.cuda.synchronize()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record(stream)
-        for _ in range(args.steps):
-            op.spmv()
-        ev1.record(stream)
-        torch.cuda.synchronize()
+        with leg_range(f"bench:plan_{plan}"):
+            ev0.record(stream)
+            for _ in range(args.steps):
+                op.spmv()
+            ev1.record(stream)
+            torch.cuda.synchronize()
         s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
         out[plan] = {"launch_us_events": round(s * 1e6, 3),
                      "gflops": round(2.0 * A.nnz / s * 1e-9, 3),
@@ -559,13 +621,14 @@ def main():
     # the same K SpMVs (the kernel-side time of one SpMV = their average)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        op.spmv()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
+    with leg_range("bench:headline"):  # the K timed launches only
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(args.steps):
+            op.spmv()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
     barrier(world)
     step_s = reduce_over_ranks(wall / args.steps, world, "max")
     ev_launch_s = ev0.elapsed_time(ev1) * 1e-3 / args.steps
@@ -578,10 +641,11 @@ def main():
     for _ in range(args.cold_steps):
         flush.sum()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        op.spmv()
-        b.record(stream)
-        torch.cuda.synchronize()
+        with leg_range("bench:headline_cold"):
+            a.record(stream)
+            op.spmv()
+            b.record(stream)
+            torch.cuda.synchronize()
         cold.append(a.elapsed_time(b) * 1e-3)
     del flush
     cold_s = reduce_over_ranks(float(np.median(cold)), world, "max") if cold else None

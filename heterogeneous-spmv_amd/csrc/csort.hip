@@ -420,8 +420,9 @@ hipError_t launch_csort_p(const DevCsort &c, const T *x, T *y, hipStream_t st) {
   return hipGetLastError();
 }
 
-// part32 (A/B, fp32 data over fp64 slots only): the column parts' row
-// partials stored as fp32 (half the partial traffic; y then rounds twice)
+// part32 (fp32 data over fp64 slots; the default, hspmv_csort_build.cpp):
+// the column parts' row partials stored as fp32 (half the partial traffic;
+// y then rounds twice on rows with entries in both parts)
 template <typename T, typename S, int U, bool NT>
 hipError_t launch_csort_u(const DevCsort &c, const T *x, T *y, hipStream_t st) {
   if constexpr (sizeof(T) == 4 && sizeof(S) == 8)

@@ -516,8 +516,16 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     s.d_cs_val = dv;
   }
   const bool direct = H == 1 && lrow.empty();
-  // row partials in the slot type (fp32 with the part32 A/B knob)
-  const int64_t part_bytes = (dtype == HSPMV_F32 && !slot32 && tn.csort_part32 == 1) ? 4 : slot_bytes;
+  // Row partials: fp32 for fp32 data (part32, the default since r06; the
+  // LDS slots stay fp64 and the finishing pass adds in fp64): half of C5's
+  // 64 MB of partial traffic, C5 98.2 -> 91.9 us, c5r 99.2 -> 94.5 (t_min,
+  // one process, profiles/r05q1/ab_part32.jsonl).  y then rounds twice on
+  // rows with entries in both column parts (the part's sum, then y):
+  // |y - y64| <= 2^-24 (sum_h |p_h| + |y64|), inside omp_spmv's own fp32
+  // error (len + 2) 2^-23 sum|a x| (tests/test_gpu_parity.py).  Tuning
+  // csort_part32 = 0 keeps fp64 partials (A/B).
+  const bool part32 = dtype == HSPMV_F32 && !slot32 && tn.csort_part32 != 0;
+  const int64_t part_bytes = part32 ? 4 : slot_bytes;
   if (!direct) {
     if ((rc = dev_alloc(&s.d_cs_part, part_bytes * (size_t)H * (size_t)m, &s.bytes))) return rc;
     if ((rc = dev_alloc(&s.d_cs_spart, slot_bytes * (size_t)std::max<int64_t>(n_slices, 1), &s.bytes)))
@@ -542,7 +550,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.prefetch = wide && dtype == HSPMV_F32;  // see `wide` above
   if (tn.csort_pf >= 0) c.prefetch = tn.csort_pf != 0;
   c.slot32 = slot32;
-  c.part32 = dtype == HSPMV_F32 && !slot32 && tn.csort_part32 == 1;
+  c.part32 = part32;
   c.wide = wide;
   c.fin_rows = tn.csort_fin_rows;
   // waves claim chunks from the workgroup's LDS queue: one process, 7

@@ -80,7 +80,7 @@ struct Tuning {
   int csort_dyn = -1;                    // chunks claimed from an LDS queue (-1: the library's choice)
   double csort_sweep_w = 0;              // column-part cost of a column per row block (0: kSweepPerRowBlock)
   double csort_slack = 0;                // widest column part / (n / H) when balancing (0: kPartSlack)
-  int csort_part32 = 0;                  // fp32 row partials over fp64 slots (fp32 data; A/B)
+  int csort_part32 = -1;                 // fp32 row partials over fp64 slots (fp32 data; -1: on, 0 off)
   int lds_pad = -1;                      // STREAM padded product buffers (-1: by row length, 0 off, 1 on)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
@@ -116,7 +116,7 @@ struct DevCsort {
   bool slot32 = false;    // fp32 LDS row slots and partials (fp32 data; A/B)
   bool wide = false;      // 16-byte entry loads (host-interleaved layout)
   bool dyn = false;       // waves claim the workgroup's chunks from an LDS queue
-  bool part32 = false;    // fp32 row partials over fp64 slots (fp32 data; A/B)
+  bool part32 = false;    // fp32 row partials over fp64 slots (fp32 data; the default)
   int32_t fin_rows = 0;   // rows per finishing-pass thread (0: 4, or the most m allows)
   int64_t m = 0;
   int32_t lds_bytes = 0;

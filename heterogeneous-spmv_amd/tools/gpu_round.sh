@@ -12,6 +12,8 @@
 #   smoke               __graft_entry__.smoke()
 #   bench[:ARGS]        python bench.py ARGS (ARGS: commas become spaces)
 #   rocprof[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS
+#   rocprofleg[:ARGS]   the same with --marker-trace --kernel-rename: kernels
+#                       reported per bench leg (bench.py's roctx ranges)
 #   kstats:CFGS         tools/gpu_kstats.sh over run_one.py (CFGS comma separated)
 #   pmc:CFG             tools/gpu_pmc_bench.sh TAG_CFG --config CFG (PMC traffic summary)
 #   ab:ARGS             tools/ab.py ARGS (commas inside ARGS: use ';' for spaces)
@@ -54,6 +56,15 @@ for step in "$@"; do
       rc=$?; echo "   rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/rocprof_bench.log; exit $rc; }
       cp $O/prof_bench/*kernel_stats.csv $O/bench_kernel_stats.csv 2>/dev/null
       head -6 $O/bench_kernel_stats.csv | cut -c1-200 ;;
+    rocprofleg)
+      echo "== rocprofleg"
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace \
+        --kernel-rename --stats --output-format csv -d $O/prof_leg -o bench -- python3 $R/bench.py ${arg//,/ }) \
+        > $O/rocprof_leg.log 2>&1
+      rc=$?; echo "   rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/rocprof_leg.log; exit $rc; }
+      grep '^{' $O/rocprof_leg.log > $O/bench_leg.json
+      cp $O/prof_leg/*kernel_stats.csv $O/bench_leg_kernel_stats.csv 2>/dev/null
+      head -12 $O/bench_leg_kernel_stats.csv | cut -c1-200 ;;
     kstats)
       run kstats 1200 bash $T/gpu_kstats.sh $TAG "${arg//,/ }" ;;
     pmc)

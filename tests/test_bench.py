@@ -241,3 +241,37 @@ def test_bench_multi_rank_path_rehearsal_on_one_gpu(tmp_path):
     assert abs(sc["efficiency"] - d["value"] / (2 * sc["n1_gflops"])) < 1e-3
     assert sc["cold_gflops"] > 0 and sc["n1_cold_gflops"] > 0
     assert abs(sc["cold_efficiency"] - sc["cold_gflops"] / (2 * sc["n1_cold_gflops"])) < 1e-3
+
+
+@pytest.mark.gpu
+def test_bench_eight_rank_orchestration_rehearsal_on_one_gpu(tmp_path):
+    """The driver's 8-GPU run is the one whose failure would be total, so its
+    orchestration is rehearsed whole: plain ``bench.py --gpus 8`` (it
+    self-launches 8 ranks) on device 0 over gloo, C2 weak scaling (8 M rows).
+    One JSON line, the y check, the halo of an interior rank (a grid line
+    from each neighbour), the overlapped gather equal to the plain one, and
+    the strong_scaling block."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONUNBUFFERED"] = "1"
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "8",
+                          "--backend", "gloo", "--same-device", "--config", "c2",
+                          "--steps", "10", "--warmup", "2", "--cold-steps", "2"],
+                         cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["scaling"] == "weak" and d["check"]["pass"] is True
+    assert d["config"]["m"] == 8_000_000 and d["config"]["parallelism"] == "row-range x8"
+    c = d["comm"]
+    assert c["bcast_x_ms"] > 0 and c["gather_y_ms"] > 0 and c["halo_x_ms"] > 0
+    # the max over ranks: an interior rank receives one grid line (1000
+    # fp64) from each of its two neighbours
+    assert c["halo_bytes_per_rank"] == 2 * 1000 * 8
+    ov = c["overlap"]
+    assert ov["chunks"] == 4 and ov["ms"] > 0 and ov["y_equal_to_plain_gather"] is True
+    assert d["cpu_baseline"] is None and d["scaling_reference"] is None
+    sc = d["strong_scaling"]
+    assert sc["n1"]["check"]["pass"] is True and sc["n1"]["m"] == 8_000_000
+    assert abs(sc["efficiency"] - d["value"] / (8 * sc["n1_gflops"])) < 1e-3
+    assert sc["cold_gflops"] > 0 and sc["n1_cold_gflops"] > 0

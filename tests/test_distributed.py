@@ -1,5 +1,5 @@
 """Multi-rank row-range partition on the CPU with gloo,
-world_size 2 and 3: each rank builds only its shard, x is broadcast from rank
+world_size 2, 3, 4 and 8 (the driver's node size): each rank builds only its shard, x is broadcast from rank
 0, the per-rank y (computed here by the oracle, the GPU's stand-in on a
 CPU-only box) is all-gathered, and the result must equal the oracle on the
 global matrix -- the same orchestration bench.py runs over RCCL."""
@@ -84,7 +84,7 @@ def _run_partition(world, use_hip):
     assert shard_nnz.max() - shard_nnz.min() <= 10     # nnz-balanced
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_row_range_partition_gloo(world):
     _run_partition(world, use_hip=False)
 
@@ -142,7 +142,7 @@ def _halo_worker(rank, world, port, config, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_halo_exchange_replaces_x_broadcast_gloo(world):
     """Banded optional mode: x distributed like the rows, each
     rank receives only its window's halo from its neighbours by send/recv,
@@ -190,7 +190,7 @@ def _overlap_worker(rank, world, port, K, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,K", [(2, 4), (3, 3), (2, 1), (4, 2)])
+@pytest.mark.parametrize("world,K", [(2, 4), (3, 3), (2, 1), (4, 2), (8, 4)])
 def test_overlapped_chunked_gather_gloo(world, K):
     """The y all-gather overlapped with the SpMV (bench.py comm
     end_to_end_overlapped_gflops): each rank's rows in K nnz-balanced chunks,

@@ -327,9 +327,11 @@ def test_config_c4_full_matrix_one_gpu():
 def test_config_c5_powerlaw_csr3_fp32():
     """BASELINE configs[4]: power-law fp32 with CSR-3 maps.  Its random
     columns make the gathers irregular, so AUTO runs the column-sorted row
-    blocks (csort: fp64 row sums, rounded once): y is checked against the
-    exact (fp64) sums to an fp32 rounding and against omp_spmv's fp32 sums
-    within their summation error.  The x-slab path (options x_slabs) stays
+    blocks (csort: fp64 row sums, stored per column part as fp32 partials and
+    added in fp64): y is checked against the exact (fp64) sums to an fp32
+    rounding of y and of each part's sum (sum_h |p_h| <= sum|a x|), and
+    against omp_spmv's fp32 sums within their summation error (the parity
+    bar).  The x-slab path (options x_slabs) stays
     available and bitwise on short rows -- AUTO streams its passes with
     STREAM (C5's 64-row groups are balanced: slab_kernel_rule), the CSR3
     tasks when forced -- and deterministic=1 keeps the row kernels."""
@@ -350,7 +352,7 @@ def test_config_c5_powerlaw_csr3_fp32():
         for it in range(12):
             op.spmv()
             yi = op.get_y() if it else y
-            assert np.all(np.abs(yi - y64) <= 2.0 ** -24 * np.abs(y64) + 1e-12 * absrow), it
+            assert np.all(np.abs(yi - y64) <= 2.0 ** -24 * (np.abs(y64) + absrow) + 1e-12 * absrow), it
             err = np.abs(yi.astype(np.float64) - y32.astype(np.float64))
             assert np.all(err <= (lens + 2) * 2.0 ** -23 * absrow + 1e-30), it
     ok = short_rows(A)
@@ -377,7 +379,7 @@ def test_config_c5r_powerlaw_rcm_csr3_fp32():
     assert info["n_split_rows"] == int((lens > 4096).sum())
     y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
     absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
-    assert np.all(np.abs(y - y64) <= 2.0 ** -24 * np.abs(y64) + 1e-12 * absrow)
+    assert np.all(np.abs(y - y64) <= 2.0 ** -24 * (np.abs(y64) + absrow) + 1e-12 * absrow)
     y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
     err = np.abs(y.astype(np.float64) - y32.astype(np.float64))
     assert np.all(err <= (lens + 2) * 2.0 ** -23 * absrow + 1e-30)
