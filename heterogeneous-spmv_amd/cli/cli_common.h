@@ -22,7 +22,10 @@
 //   --plan aligned|packed|ssr   CSR-3 wave-task plan (hspmv_options.csr3_plan;
 //                       ssr = one workgroup per super-super-row, the
 //                       reference's cuSpMV_3 mapping)
-//   --deterministic     only kernels whose y is bit-identical run to run
+//   --deterministic     only the ordered row kernels (omp_spmv's order; y
+//                       bit-identical run to run)
+//   --reproducible      y bit-identical run to run, the column-sorted kernel
+//                       allowed with fixed-point row sums
 //   --dump-y PATH       write y as raw binary (dtype) for external checks
 //   --no-check          skip the serial CPU check
 #pragma once
@@ -48,7 +51,7 @@ struct Options {
   unsigned lanes = 0;
   bool nt = false;
   int plan = HSPMV_CSR3_PLAN_AUTO;
-  bool deterministic = false;
+  int deterministic = 0;  // hspmv_options.deterministic
   bool check = true;
   std::string dump_y;
   std::string params = "mi355x";
@@ -103,7 +106,9 @@ inline bool parse_options(int argc, char **argv, int first, Options &o) {
       else if (!strcmp(v, "ssr")) o.plan = HSPMV_CSR3_PLAN_SSR;
       else { fprintf(stderr, "bad --plan %s\n", v); return false; }
     } else if (a == "--deterministic") {
-      o.deterministic = true;
+      o.deterministic = HSPMV_DETERMINISTIC_ORDERED;
+    } else if (a == "--reproducible") {
+      o.deterministic = HSPMV_DETERMINISTIC_REPRODUCIBLE;
     } else if (a == "--no-check") {
       o.check = false;
     } else if (a == "--dump-y") {
@@ -200,7 +205,7 @@ inline int run_and_report(const hspmv_csr_buf &A, const hspmv_csr3_buf *maps, in
   opt.devices = gpus > 1 ? devs.data() : nullptr;  // row-range shards over RCCL
   opt.n_devices = gpus > 1 ? gpus : 0;
   opt.csr3_plan = o.plan;
-  opt.deterministic = o.deterministic ? 1 : 0;
+  opt.deterministic = o.deterministic;
   if (hspmv_create_ex(&h, &view, mv.n_ssr > 0 ? &mv : nullptr, &opt) != HSPMV_OK)
     return die("hspmv_create_ex");
   std::vector<double> x64;

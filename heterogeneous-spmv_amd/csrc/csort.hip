@@ -160,37 +160,30 @@ __device__ __forceinline__ void load_entries(const void *__restrict__ ent, const
   }
 }
 
-// S: the LDS row-slot / partial-sum type (double; float only for fp32 data,
-// an A/B variant with half the LDS per row).
-template <typename T, typename S, typename P, int U, bool NT, bool PF, bool WIDE>
-__global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
-    int32_t H, int64_t m, int32_t direct, const int32_t *__restrict__ blk_c,
-    const int32_t *__restrict__ blk_r, const int32_t *__restrict__ blk_v,
-    const int32_t *__restrict__ vslice, const int32_t *__restrict__ cbase,
-    const void *__restrict__ ent, const T *__restrict__ val, const T *__restrict__ x,
-    P *__restrict__ part, S *__restrict__ spart, T *__restrict__ y,
-    unsigned long long *__restrict__ trace, int32_t dyn) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int32_t next_chunk;  // dyn: the workgroup's chunk queue head
-  S *acc = reinterpret_cast<S *>(smem);
+// Reproducible (fixed-point) slots, FIXP: each product v' x (v' = v 2^rexp,
+// scaled per row on the host so that |v'| < 1) is rounded ONCE to an integer
+// at scale 2^E, E = kCsortFixBits - xexp (|x| < 2^xexp): one fma with the
+// 1.5 * 2^52 rounding constant gives rint(v' x 2^E) in the low mantissa
+// bits, and the int64 difference of the bit patterns is that integer
+// (|q| < 2^50).  Integer adds are associative, so the slot's sum -- and y --
+// is the same bits whatever order the LDS atomics land in (ds_add_u64 costs
+// what ds_add_f64 does: profiles/r03/ab_c5_lds_add_ablation.jsonl).
+__device__ __forceinline__ long long fix_q(double v, double xs) {
+  const double r = __builtin_fma(v, xs, 0x1.8p52);
+  return (long long)(__builtin_bit_cast(unsigned long long, r) - 0x4338000000000000ull);
+}
+
+// The chunks of one workgroup (see hspmv_csort).  FIXP: integer slots (the
+// products rounded by fix_q at scale 2^E); otherwise S slots (ds_add_f64,
+// or ds_add_f32 with fp32 slots).
+template <typename T, typename S, int U, bool NT, bool PF, bool WIDE, bool FIXP>
+__device__ __forceinline__ int32_t csort_chunks(int32_t c0, int32_t c1, int wid, int lane, int32_t dyn,
+                                                int32_t *next_chunk, const int32_t *__restrict__ cbase,
+                                                const void *__restrict__ ent, const T *__restrict__ val,
+                                                const T *__restrict__ x, void *slots, int32_t E) {
   constexpr int NW = kCsortThreads / kWave;
-  const int b = blockIdx.x;
-  unsigned long long *tr = trace ? trace + (int64_t)b * kCsortTraceSlots : nullptr;
-  if (tr && threadIdx.x == 0) {  // diagnostic builds only (DevCsort.trace)
-    tr[0] = __builtin_amdgcn_s_memrealtime();
-    tr[2] = __builtin_amdgcn_s_getreg((31 << 11) | 20) |
-            ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32);
-  }
-  const int h = b % H;  // the column part; its rows: the part's own row block
-  const int32_t c0 = blk_c[b], c1 = blk_c[b + 1];
-  const int32_t r0 = blk_r[2 * b], r1 = blk_r[2 * b + 1];
-  const int32_t v0 = blk_v[b], v1 = blk_v[b + 1];
-  const int32_t nr = r1 - r0, nv = v1 - v0;
-  for (int32_t i = threadIdx.x; i <= nr + nv; i += kCsortThreads) acc[i] = S(0);  // + dummy
-  if (threadIdx.x == 0) next_chunk = c0 + NW;
-  __syncthreads();
-  if (tr && threadIdx.x == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+  S *acc = reinterpret_cast<S *>(slots);
+  unsigned long long *acq = reinterpret_cast<unsigned long long *>(slots);
   uint32_t ix[U];
   T vv[U];
 #if HSPMV_CSORT_ABL == 2 || HSPMV_CSORT_ABL == 3
@@ -211,7 +204,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     int32_t cn = c + NW;
     if (dyn) {
       int32_t got = 0;
-      if (lane == 0) got = atomicAdd(&next_chunk, 1);
+      if (lane == 0) got = atomicAdd(next_chunk, 1);
       cn = __builtin_amdgcn_readfirstlane(got);
     }
     ++cn_done;
@@ -242,24 +235,29 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     if (!seg) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        S pr;
-        if constexpr (sizeof(T) == 4 && sizeof(S) == 8)
-          pr = (double)vvc[u] * (double)xv[u];  // exact
-        else
-          pr = (S)(vvc[u] * xv[u]);  // omp_spmv's rounded product
+        if constexpr (FIXP) {
+          const long long q = fix_q((double)vvc[u], __builtin_ldexp((double)xv[u], E));
+          atomicAdd(&acq[ixc[u] >> 16], (unsigned long long)q);
+        } else {
+          S pr;
+          if constexpr (sizeof(T) == 4 && sizeof(S) == 8)
+            pr = (double)vvc[u] * (double)xv[u];  // exact
+          else
+            pr = (S)(vvc[u] * xv[u]);  // omp_spmv's rounded product
 #if HSPMV_CSORT_ABL == 1
-        if constexpr (sizeof(S) == 8)
-          atomicAdd(reinterpret_cast<unsigned long long *>(&acc[ixc[u] >> 16]),
-                    (unsigned long long)__builtin_bit_cast(long long, pr));
-        else
-          atomicAdd(&acc[ixc[u] >> 16], pr);
+          if constexpr (sizeof(S) == 8)
+            atomicAdd(reinterpret_cast<unsigned long long *>(&acc[ixc[u] >> 16]),
+                      (unsigned long long)__builtin_bit_cast(long long, pr));
+          else
+            atomicAdd(&acc[ixc[u] >> 16], pr);
 #elif HSPMV_CSORT_ABL == 2
-        sink += pr + (S)(ixc[u] >> 16);
+          sink += pr + (S)(ixc[u] >> 16);
 #elif HSPMV_CSORT_ABL == 3
-        sink += pr * acc[ixc[u] >> 16];
+          sink += pr * acc[ixc[u] >> 16];
 #else
-        atomicAdd(&acc[ixc[u] >> 16], pr);
+          atomicAdd(&acc[ixc[u] >> 16], pr);
 #endif
+        }
       }
     } else {
       // Segmented chunk: the host found rows whose entries crowd one
@@ -272,11 +270,6 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
       // per run.
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        S v;
-        if constexpr (sizeof(T) == 4 && sizeof(S) == 8)
-          v = (double)vvc[u] * (double)xv[u];
-        else
-          v = (S)(vvc[u] * xv[u]);
         const uint32_t sl = ixc[u] >> 16;
         // runs = maximal stretches of lanes with one slot; run id = the
         // number of run starts up to this lane (ballot + mbcnt)
@@ -286,28 +279,146 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
         const uint32_t rid = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32),
                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u)) +
                              (start ? 1u : 0u);
-        v = seg_scan(v, rid);
-        if (lane == kWave - 1 || ((msk >> (lane + 1)) & 1ull)) atomicAdd(&acc[sl], v);
+        const bool last = lane == kWave - 1 || ((msk >> (lane + 1)) & 1ull);
+        if constexpr (FIXP) {
+          unsigned long long q = (unsigned long long)fix_q((double)vvc[u], __builtin_ldexp((double)xv[u], E));
+          q = seg_scan(q, rid);  // integer: the same sum in any association
+          if (last) atomicAdd(&acq[sl], q);
+        } else {
+          S v;
+          if constexpr (sizeof(T) == 4 && sizeof(S) == 8)
+            v = (double)vvc[u] * (double)xv[u];
+          else
+            v = (S)(vvc[u] * xv[u]);
+          v = seg_scan(v, rid);
+          if (last) atomicAdd(&acc[sl], v);
+        }
       }
     }
     c = cn;
   }
 #if HSPMV_CSORT_ABL == 2 || HSPMV_CSORT_ABL == 3
-  if (sink != S(0)) atomicAdd(&acc[nr + nv], sink);  // the dummy slot: keeps the products live
+  if (sink != S(0)) atomicAdd(&acc[0], sink * S(0));  // keeps the products live (adds 0)
 #endif
+  return cn_done;
+}
+
+// A slot's value: S slots as they are; fixed-point slots scaled back by
+// 2^-(E + rexp) -- the int64 -> double conversion and the scaling round
+// deterministically.
+template <typename S, bool FIXP>
+__device__ __forceinline__ S slot_value(const void *slots, int32_t i, int32_t e) {
+  if constexpr (FIXP)
+    return (S)__builtin_ldexp((double)(long long)reinterpret_cast<const unsigned long long *>(slots)[i], -e);
+  else
+    return reinterpret_cast<const S *>(slots)[i];
+}
+
+// The max exponent of |x| the workgroup's fixed-point scale comes from,
+// reduced by each wave from the pre-pass's per-block maxima.
+__device__ __forceinline__ int32_t wave_xexp(const int32_t *__restrict__ xexp_part, int32_t n, int lane) {
+  int32_t e = -0x40000000;
+  for (int32_t i = lane; i < n; i += kWave) e = max(e, xexp_part[i]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) e = max(e, __shfl_xor(e, off, kWave));
+  return __builtin_amdgcn_readfirstlane(e);
+}
+
+// S: the LDS row-slot / partial-sum type (double; float only for fp32 data,
+// an A/B variant with half the LDS per row).  FIX: reproducible fixed-point
+// slots (DevCsort.fixed), falling back to S slots for an x with a non-finite
+// entry (whose rows are then +-Inf / NaN in any order).
+template <typename T, typename S, typename P, int U, bool NT, bool PF, bool WIDE, bool FIX>
+__global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
+    int32_t H, int64_t m, int32_t direct, const int32_t *__restrict__ blk_c,
+    const int32_t *__restrict__ blk_r, const int32_t *__restrict__ blk_v,
+    const int32_t *__restrict__ vslice, const int32_t *__restrict__ cbase,
+    const void *__restrict__ ent, const T *__restrict__ val, const T *__restrict__ x,
+    P *__restrict__ part, S *__restrict__ spart, T *__restrict__ y,
+    unsigned long long *__restrict__ trace, int32_t dyn, const int16_t *__restrict__ rexp,
+    const int16_t *__restrict__ sexp, const int32_t *__restrict__ xexp_part, int32_t n_xexp) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int32_t next_chunk;  // dyn: the workgroup's chunk queue head
+  static_assert(!FIX || sizeof(S) == 8, "fixed-point slots are 8 bytes");
+  constexpr int NW = kCsortThreads / kWave;
+  const int b = blockIdx.x;
+  unsigned long long *tr = trace ? trace + (int64_t)b * kCsortTraceSlots : nullptr;
+  if (tr && threadIdx.x == 0) {  // diagnostic builds only (DevCsort.trace)
+    tr[0] = __builtin_amdgcn_s_memrealtime();
+    tr[2] = __builtin_amdgcn_s_getreg((31 << 11) | 20) |
+            ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32);
+  }
+  const int h = b % H;  // the column part; its rows: the part's own row block
+  const int32_t c0 = blk_c[b], c1 = blk_c[b + 1];
+  const int32_t r0 = blk_r[2 * b], r1 = blk_r[2 * b + 1];
+  const int32_t v0 = blk_v[b], v1 = blk_v[b + 1];
+  const int32_t nr = r1 - r0, nv = v1 - v0;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+  // FIX: the SpMV's x exponent (every wave reduces the pre-pass's maxima:
+  // no LDS, no extra barrier); a non-finite x -> the S-slot fallback
+  int32_t xe = 0;
+  if constexpr (FIX) xe = wave_xexp(xexp_part, n_xexp, lane);
+  const bool fixp = FIX && xe != kCsortXexpNonFinite;  // uniform over the grid
+  const int32_t E = fixp ? kCsortFixBits - xe : 0;
+  for (int32_t i = threadIdx.x; i <= nr + nv; i += kCsortThreads)  // + dummy; 0 = +0.0 = integer 0
+    reinterpret_cast<S *>(smem)[i] = S(0);
+  if (threadIdx.x == 0) next_chunk = c0 + NW;
+  __syncthreads();
+  if (tr && threadIdx.x == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
+  int32_t cn_done;
+  if (fixp)
+    cn_done = csort_chunks<T, S, U, NT, PF, WIDE, FIX>(c0, c1, wid, lane, dyn, &next_chunk, cbase, ent, val,
+                                                       x, smem, E);
+  else
+    cn_done = csort_chunks<T, S, U, NT, PF, WIDE, false>(c0, c1, wid, lane, dyn, &next_chunk, cbase, ent,
+                                                         val, x, smem, 0);
   if (tr && lane == 0) {  // this wave's end and chunk count (its LDS adds issued)
     tr[4 + wid] = __builtin_amdgcn_s_memrealtime();
     tr[4 + NW + wid] = (unsigned long long)cn_done;
   }
   __syncthreads();
   if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+  // FIX: the slot of row r is at scale 2^(E + rexp[r]) (the fallback: 2^rexp[r])
+  auto val_at = [&](int32_t i, int32_t e) -> S {
+    if constexpr (FIX) {
+      if (fixp) return slot_value<S, true>(smem, i, E + e);
+      return (S)__builtin_ldexp((double)reinterpret_cast<const S *>(smem)[i], -e);
+    } else {
+      return slot_value<S, false>(smem, i, 0);
+    }
+  };
   if (direct) {  // one column part, no long rows: y straight from the slots
-    for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) y[r0 + i] = (T)acc[i];
+    for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads)
+      y[r0 + i] = (T)val_at(i, FIX ? (int32_t)rexp[r0 + i] : 0);
     return;
   }
   P *out = part + (int64_t)h * m + r0;
-  for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) out[i] = (P)acc[i];
-  for (int32_t i = threadIdx.x; i < nv; i += kCsortThreads) spart[vslice[v0 + i]] = acc[nr + i];
+  for (int32_t i = threadIdx.x; i < nr; i += kCsortThreads) out[i] = (P)val_at(i, FIX ? (int32_t)rexp[r0 + i] : 0);
+  for (int32_t i = threadIdx.x; i < nv; i += kCsortThreads) {
+    const int32_t sl = vslice[v0 + i];
+    spart[sl] = val_at(nr + i, FIX ? (int32_t)sexp[sl] : 0);
+  }
+}
+
+// Pre-pass of the fixed-point csort (one per SpMV, before it): per block the
+// max frexp exponent of |x| (|x| < 2^e), kCsortXexpNonFinite if the block saw
+// an Inf or a NaN; zeros do not count.  Every csort wave max-reduces the
+// n_xexp block results itself (wave_xexp).
+template <typename T>
+__global__ __launch_bounds__(256) void hspmv_csort_xexp(int64_t n, const T *__restrict__ x,
+                                                        int32_t *__restrict__ out) {
+  __shared__ int32_t wmax[4];
+  int32_t e = -0x40000000;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double v = __builtin_fabs((double)x[i]);
+    if (!(v <= 1.7976931348623157e308)) e = kCsortXexpNonFinite;  // Inf, NaN
+    else if (v != 0.0) e = max(e, __builtin_amdgcn_frexp_exp(v));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) e = max(e, __shfl_xor(e, off, kWave));
+  if ((threadIdx.x & (kWave - 1)) == 0) wmax[threadIdx.x >> 6] = e;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
 }
 
 // y[r] = part[r] + part[m + r] + ... (parts in order), except long rows:
@@ -379,10 +490,21 @@ void launch_finish(const DevCsort &c, const P *part, const S *spart, T *y, hipSt
 
 template <typename T, typename S, typename P, int U, bool NT, bool PF, bool WIDE>
 void launch_csort_main(const DevCsort &c, const T *x, P *part, S *spart, T *y, hipStream_t st) {
-  hipLaunchKernelGGL((hspmv_csort<T, S, P, U, NT, PF, WIDE>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
+  if constexpr (sizeof(S) == 8) {
+    if (c.fixed) {
+      hipLaunchKernelGGL((hspmv_csort_xexp<T>), dim3((unsigned)c.n_xexp), dim3(256), 0, st, c.n_x, x,
+                         c.xexp_part);
+      hipLaunchKernelGGL((hspmv_csort<T, S, P, U, NT, PF, WIDE, true>), dim3((unsigned)c.n_wg),
+                         dim3(kCsortThreads), (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r,
+                         c.blk_v, c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y,
+                         c.trace, c.dyn ? 1 : 0, c.rexp, c.sexp, c.xexp_part, c.n_xexp);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((hspmv_csort<T, S, P, U, NT, PF, WIDE, false>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
                      (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
                      c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y,
-                     c.trace, c.dyn ? 1 : 0);
+                     c.trace, c.dyn ? 1 : 0, nullptr, nullptr, nullptr, 0);
 }
 
 template <typename T, typename S, typename P, int U, bool NT>
@@ -445,6 +567,8 @@ hipError_t launch_csort_nt(const DevCsort &c, const T *x, T *y, hipStream_t st) 
 hipError_t launch_csort(const DevCsort &c, int dtype, const void *x, void *y, hipStream_t st) {
   if (c.m == 0) return hipSuccess;
   if (c.n_wg <= 0 || c.lds_bytes > kCsortMaxLds) return hipErrorInvalidValue;
+  if (c.fixed && (c.slot32 || !c.rexp || !c.xexp_part || c.n_xexp <= 0 || c.n_xexp > kCsortXexpBlocks))
+    return hipErrorInvalidValue;
   if (dtype == 1) {
     if (c.slot32) return hipErrorInvalidValue;
     return c.nontemporal ? launch_csort_nt<double, double, true>(c, (const double *)x, (double *)y, st)

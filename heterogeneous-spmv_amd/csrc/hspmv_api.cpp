@@ -419,7 +419,7 @@ static int fill_info(hspmv_handle *h, hspmv_info *out) {
   out->placement_pick = s.place_pick;
   for (size_t k = 0; k < s.place_us.size() && k < 8; ++k) out->placement_us[k] = s.place_us[k];
   out->deterministic = 1;
-  for (auto &sh : h->shards) out->deterministic &= sh.plan.kernel == kCsort ? 0 : 1;
+  for (auto &sh : h->shards) out->deterministic &= (sh.plan.kernel == kCsort && !sh.dp.cs.fixed) ? 0 : 1;
   // the maps-driven plans need maps; a CSR matrix whose heavy 64-row groups
   // sent it to the CSR3 kernel runs build_tasks' row groups
   out->csr3_plan = s.plan.kernel != kCsr3 ? 0
@@ -432,6 +432,7 @@ static int fill_info(hspmv_handle *h, hspmv_info *out) {
   out->slab_kernel_rule = s.heavy_frac < 0 ? 0 : (s.A.slab_stream ? 2 : 1);
   out->heavy_group_frac = s.heavy_frac < 0 ? 0.0 : s.heavy_frac;
   out->lds_pad = s.plan.lds_pad ? 1 : 0;
+  out->csort_fixed_point = s.plan.kernel == kCsort && s.dp.cs.fixed ? 1 : 0;
   for (auto &sh : h->shards)
     if (sh.plan.kernel == kCsort) {
       out->csort_chunks += sh.csort_chunks;

@@ -26,7 +26,8 @@ namespace hspmv {
 // Padding entries add 0 * x[base] to a dummy slot that is never read.
 // Auto: HBM-resident matrices with irregular gathers from an x beyond the
 // L1 (> 256 KiB; it replaced the x-slab rule: C5 264 -> ~110 us), unless the
-// handle asks for deterministic sums (the slots add in atomic order);
+// handle asks for ordered sums (deterministic = 1: the slots add in atomic
+// order); deterministic = 2 builds it with fixed-point (reproducible) slots;
 // HSPMV_KERNEL_CSORT forces it, Tuning.csort = -1 turns auto off,
 // Tuning.csort_parts = 1/2/4 sets the column parts, csort_u = 4/8/16 the
 // chunk.  The row blocks are capped by the device's LDS per workgroup.
@@ -148,6 +149,47 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     lcs.push_back((int32_t)slice_k.size());
   }
   const int64_t n_slices = (int64_t)slice_k.size();
+  // Reproducible (fixed-point) slots (Tuning.deterministic == 2, csort.hip
+  // fix_q): every value of row r is stored scaled by 2^rexp[r], exactly (a
+  // power of two), so that the row's |v'| < 2^-extra: rexp = -(ilogb max|v| +
+  // 1) - extra, extra = ceil(log2 len) - 12 for a row kept whole over 4096
+  // nonzeros (HSPMV_FLAG_NO_SPLIT), else 0 -- every product then rounds to an
+  // integer below 2^kCsortFixBits and a slot of <= 4096 of them stays below
+  // 2^62.  A value that the scaling takes below the type's normal range loses
+  // bits only below the products' rounding unit (2^-kCsortFixBits of the
+  // row's largest).
+  const bool fixed = tn.deterministic == 2 && !slot32;
+  std::vector<int16_t> rexp(fixed ? (size_t)m : 0, 0), sexp;
+  if (fixed) {
+    for (int64_t r = 0; r < m; ++r) {
+      double mx = 0.0;
+      for (int32_t k = rp[r]; k < rp[r + 1]; ++k) {
+        const double v = dtype == HSPMV_F32 ? (double)static_cast<const float *>(val)[k]
+                                            : static_cast<const double *>(val)[k];
+        mx = std::max(mx, std::fabs(v));
+      }
+      if (!(mx > 0.0) || !std::isfinite(mx)) continue;  // empty / zero rows (non-finite values: as 2^0)
+      const int64_t len = rp[r + 1] - rp[r];
+      int extra = 0;  // (a sliced row's slots hold kCsortSlice <= 4096 products each)
+      while (len <= long_t && ((int64_t)4096 << extra) < len) ++extra;
+      rexp[(size_t)r] = (int16_t)(-(std::ilogb(mx) + 1) - extra);
+    }
+    sexp.resize((size_t)std::max<int64_t>(n_slices, 1), 0);
+    for (size_t j = 0; j + 1 < lcs.size(); ++j)
+      for (int32_t sl = lcs[j]; sl < lcs[j + 1]; ++sl) sexp[(size_t)sl] = rexp[(size_t)lrow[j]];
+  }
+  // the (scaled) value of nonzero k of row r
+  auto value_f32 = [&](uint32_t k, int64_t r) -> uint32_t {
+    float v = static_cast<const float *>(val)[k];
+    if (fixed) v = std::ldexp(v, rexp[(size_t)r]);
+    uint32_t b;
+    memcpy(&b, &v, 4);
+    return b;
+  };
+  auto value_f64 = [&](uint32_t k, int64_t r) -> double {
+    const double v = static_cast<const double *>(val)[k];
+    return fixed ? std::ldexp(v, rexp[(size_t)r]) : v;
+  };
   // Row blocks PER COLUMN PART.  Part h is a fixed slice of x, [pb[h],
   // pb[h+1]) (above), and workgroup j works on part
   // j % H: under round-robin dispatch (workgroup j on XCD j % 8;
@@ -347,6 +389,10 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   blk_v[(size_t)G] = (int32_t)vslice.size();
   if (tot_chunks * C >= (int64_t)1 << 40 || tot_chunks >= INT32_MAX) return HSPMV_OK;
   const int64_t tot = tot_chunks * C;
+  std::vector<int32_t> slice_row_of((size_t)n_slices, 0);
+  for (size_t j = 0; j + 1 < lcs.size(); ++j)
+    for (int32_t sl = lcs[j]; sl < lcs[j + 1]; ++sl) slice_row_of[(size_t)sl] = lrow[j];
+  auto slice_row = [&](int32_t sl) -> int64_t { return slice_row_of[(size_t)sl]; };
   // pass 2: the device arrays
   std::vector<int32_t> cbase((size_t)std::max<int64_t>(tot_chunks, 1), 0);
   std::vector<uint32_t> idx;
@@ -373,6 +419,11 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
         for (int64_t b = t; b < G; b += nt) {
           auto &E = ents[(size_t)b];
           const uint32_t dummy = (uint32_t)(nslots[(size_t)b] - 1);
+          const int32_t br0 = wg_rows[(size_t)(2 * b)], bnr = wg_rows[(size_t)(2 * b + 1)] - br0;
+          const auto &bsl = wg_sl[(size_t)b];
+          auto row_of = [&](uint32_t slot) -> int64_t {  // source row of a slot (fixed-point scale)
+            return (int32_t)slot < bnr ? (int64_t)br0 + slot : slice_row(bsl[slot - bnr]);
+          };
           const int64_t cfirst = blk_c[(size_t)b];
           // entry q of a chunk (lane q % 64, u = q / 64) is stored at q, or,
           // for 16-byte loads, interleaved so that one load brings the lane
@@ -465,19 +516,21 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
               const int64_t o = ch * C + at(q, dtype == HSPMV_F32 ? 2 : 4);
               const int64_t ov = ch * C + at(q, 2);
               uint32_t ix = dummy << 16;  // padding: 0 * x[base] into the dummy slot
-              const void *vp = nullptr;
-              if (q < ne) {
-                const CsEnt &e = src[q];
-                ix = (e.slot << 16) | (e.col - c0);
-                vp = (const char *)val + sv * (size_t)e.k;
-              }
               if (dtype == HSPMV_F32) {
                 uint32_t vb = 0;
-                if (vp) memcpy(&vb, vp, 4);
+                if (q < ne) {
+                  const CsEnt &e = src[q];
+                  ix = (e.slot << 16) | (e.col - c0);
+                  vb = value_f32(e.k, row_of(e.slot));
+                }
                 rec[(size_t)o] = ((uint64_t)vb << 32) | ix;
               } else {
+                if (q < ne) {
+                  const CsEnt &e = src[q];
+                  ix = (e.slot << 16) | (e.col - c0);
+                  val64[(size_t)ov] = value_f64(e.k, row_of(e.slot));
+                }
                 idx[(size_t)o] = ix;
-                if (vp) memcpy(&val64[(size_t)ov], vp, 8);
               }
             }
           });
@@ -535,6 +588,12 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     if ((rc = up(&s.d_cs_mask, mask)) || (rc = up(&s.d_cs_long_row, lrow)) || (rc = up(&s.d_cs_long_cs, lcs)))
       return rc;
   }
+  int32_t n_xexp = 0;
+  if (fixed) {
+    if ((rc = up(&s.d_cs_rexp, rexp)) || (rc = up(&s.d_cs_sexp, sexp))) return rc;
+    n_xexp = (int32_t)std::min<int64_t>(kCsortXexpBlocks, std::max<int64_t>(1, (n + 256 * 32 - 1) / (256 * 32)));
+    if ((rc = dev_alloc(&s.d_cs_xexp, 4 * (size_t)n_xexp, &s.bytes))) return rc;
+  }
   // (An in-launch combine -- write-through partials, an arrival counter per
   // row block, the last arriver adding the parts -- measured slower than
   // the finishing launch: C5 114.8 vs 107.3 us, profiles/r02s_*.)
@@ -553,6 +612,12 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.part32 = part32;
   c.wide = wide;
   c.fin_rows = tn.csort_fin_rows;
+  c.fixed = fixed;
+  c.rexp = s.d_cs_rexp;
+  c.sexp = s.d_cs_sexp;
+  c.xexp_part = s.d_cs_xexp;
+  c.n_xexp = n_xexp;
+  c.n_x = n;
   // waves claim chunks from the workgroup's LDS queue: one process, 7
   // rounds (profiles/r05c/ab_csort_dyn.jsonl): C5 106.9 -> 101.9 us median,
   // c5r 107.3 -> 104.9, fp64 C5 flat (175.7 -> 174.7)
@@ -589,8 +654,10 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   const double part_traffic =
       direct ? 0.0
              : 2.0 * ((double)part_bytes * (double)H * (double)m + (double)slot_bytes * (double)n_slices);
+  // (fixed-point: + the x pre-pass and the row scales)
+  const double fix_traffic = fixed ? (double)n * (double)sv + 2.0 * (double)H * (double)m : 0.0;
   s.csort_format_bytes = (double)tot * (double)(4 + sv) + 4.0 * (double)tot_chunks + xb + part_traffic +
-                         (double)sv * (double)m;
+                         (double)sv * (double)m + fix_traffic;
   s.A.has_csort = true;
   return HSPMV_OK;
 }

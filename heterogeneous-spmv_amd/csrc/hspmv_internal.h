@@ -57,7 +57,7 @@ struct Tuning {
   int csort_parts = 0;      // 0 auto, 1/2/4
   int csort_u = 0;          // 0 auto, 4/8/16
   int stream_waves = 0;     // 0 auto, 1/2/4
-  int deterministic = 0;    // 1: only kernels whose y bits never depend on scheduling
+  int deterministic = 0;    // 1: ordered row kernels (omp_spmv's order); 2: reproducible (fixed-point csort allowed)
   int placement_trials = 0; // 0/1 off, K <= 8 array sets
   int ssr_w = 0;            // SSR plan waves per workgroup (0: ssr_waves(); A/B)
   int ssr_align = -1;       // SSR plan wave cut: 2 row-granular nnz balance (-1: default), 0 super-rows, 1 aligned pieces
@@ -109,6 +109,13 @@ constexpr int kCsortMaxLds = 160 * 1024;
 // after the slot-zeroing barrier, then per wave: its end (after its last
 // chunk), then per wave: the chunks it ran} (s_memrealtime, 100 MHz).
 constexpr int kCsortTraceSlots = 4 + 2 * (kCsortThreads / 64);
+// Fixed-point slots: every product rounds to an integer below 2^kCsortFixBits
+// (values scaled to |v'| < 1 per row, x to |x'| < 2^kCsortFixBits), so a slot
+// of <= 4096 products stays below 2^62; the pre-pass runs kCsortXexpBlocks
+// workgroups at most.
+constexpr int kCsortFixBits = 50;
+constexpr int kCsortXexpBlocks = 256;
+constexpr int32_t kCsortXexpNonFinite = 0x7fffffff;
 struct DevCsort {
   int32_t n_wg = 0, H = 1, u = 16, direct = 0, n_long = 0;
   bool nontemporal = true;
@@ -117,6 +124,16 @@ struct DevCsort {
   bool wide = false;      // 16-byte entry loads (host-interleaved layout)
   bool dyn = false;       // waves claim the workgroup's chunks from an LDS queue
   bool part32 = false;    // fp32 row partials over fp64 slots (fp32 data; the default)
+  // Reproducible (fixed-point) row sums (hspmv_options.deterministic = 2):
+  // the slots are int64 sums of each product rounded to an integer at scale
+  // 2^(kCsortFixBits - xexp - rexp[row]); xexp = the max exponent of |x|,
+  // found per SpMV by hspmv_csort_xexp into xexp_part[n_xexp] (csort.hip)
+  bool fixed = false;
+  const int16_t *rexp = nullptr;  // per row: the exponent its values were scaled by (2^rexp)
+  const int16_t *sexp = nullptr;  // per long-row slice: its row's rexp
+  int32_t *xexp_part = nullptr;   // per pre-pass block: max frexp exponent of |x| (INT32_MAX: non-finite)
+  int32_t n_xexp = 0;
+  int64_t n_x = 0;                // x entries the pre-pass reads
   int32_t fin_rows = 0;   // rows per finishing-pass thread (0: 4, or the most m allows)
   int64_t m = 0;
   int32_t lds_bytes = 0;

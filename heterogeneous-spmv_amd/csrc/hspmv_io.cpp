@@ -233,7 +233,7 @@ extern "C" {
 
 const char *hspmv_last_error(void) { return g_err.c_str(); }
 
-const char *hspmv_version(void) { return "hspmv 1.0 (gfx950)"; }
+const char *hspmv_version(void) { return "hspmv 1.1 (gfx950)"; }
 
 void hspmv_free_csr(hspmv_csr_buf *A) {
   if (!A) return;

@@ -30,9 +30,12 @@ int tuning_from_options(const hspmv_options *o, Tuning *t) {
       (v.stream_waves && v.stream_waves != 1 && v.stream_waves != 2 && v.stream_waves != 4) ||
       v.task_nnz < 0 || v.x_dict_cap < 0 || v.placement_trials < 0 || v.placement_trials > 8)
     return set_error(HSPMV_E_INVALID, "hspmv_options: value out of range");
-  if (v.deterministic && ((v.flags & 0xFu) == kCsort || v.csort > 0))
+  if (v.deterministic < 0 || v.deterministic > HSPMV_DETERMINISTIC_REPRODUCIBLE)
+    return set_error(HSPMV_E_INVALID, "deterministic %d unknown", v.deterministic);
+  if (v.deterministic == HSPMV_DETERMINISTIC_ORDERED && ((v.flags & 0xFu) == kCsort || v.csort > 0))
     return set_error(HSPMV_E_INVALID, "the column-sorted kernel (HSPMV_KERNEL_CSORT, csort = 1) "
-                                      "is not deterministic");
+                                      "does not sum in omp_spmv's order (deterministic = 2 runs it "
+                                      "with reproducible fixed-point sums)");
   t->csr3_plan = v.csr3_plan;
   t->task_nnz = v.task_nnz;
   t->x_windows = v.x_windows < 0 ? -1 : 0;
@@ -44,7 +47,7 @@ int tuning_from_options(const hspmv_options *o, Tuning *t) {
   t->csort_parts = v.csort_parts;
   t->csort_u = v.csort_chunk_u;
   t->stream_waves = v.stream_waves;
-  t->deterministic = v.deterministic ? 1 : 0;
+  t->deterministic = v.deterministic;
   t->placement_trials = v.placement_trials;
   return HSPMV_OK;
 }
@@ -87,6 +90,7 @@ void tuning_from_env(Tuning *t) {
   if (const char *e = getenv("HSPMV_CSORT_SWEEP")) t->csort_sweep_w = atof(e);
   if (const char *e = getenv("HSPMV_CSORT_SLACK")) t->csort_slack = atof(e);
   geti("HSPMV_CSORT_PART32", &t->csort_part32);
+  geti("HSPMV_DETERMINISTIC", &t->deterministic);
   geti("HSPMV_LDS_PAD", &t->lds_pad);
   geti("HSPMV_STREAM_W", &t->stream_waves);
   geti("HSPMV_PLACEMENT", &t->placement_trials);

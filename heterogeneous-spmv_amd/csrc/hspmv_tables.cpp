@@ -689,16 +689,18 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
     const int cm = s.tune.csort;  // -1 off, 0 auto, 1 whenever it can be built
     const double sv = (double)dtype_size(dtype);
     const double footprint = (double)rp[m] * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv;
-    // a deterministic handle never builds the csort tables: the planner
-    // would pick kCsort whenever they exist (plan_launch)
-    bool want = !s.tune.deterministic && (kf == kCsort || cm == 1);
+    // an ordered handle (deterministic = 1) never builds the csort tables:
+    // the planner would pick kCsort whenever they exist (plan_launch); a
+    // reproducible one (2) builds them with fixed-point slots
+    const bool ordered = s.tune.deterministic == 1;
+    bool want = !ordered && (kf == kCsort || cm == 1);
     // Scattered gathers from an x the L1 cannot hold go to the L2 one line
     // per nonzero, at its request rate, whatever the L2's capacity: until r04
     // the rule also asked for x beyond an XCD's 4 MiB L2, which kept fp32
     // `mix` (x = 3.8 MiB, random columns within +-4000) on the CSR3 kernel
     // at 90.8 us against csort's 62.5 (profiles/r04/auto_regret_f32.jsonl);
     // x of a few L1s (the zoo's `tall`, 16-32 KiB) stays on the row kernels.
-    if (!want && kf == kAuto && cm == 0 && !s.tune.deterministic && s.tune.x_slabs == 0 &&
+    if (!want && kf == kAuto && cm == 0 && !ordered && s.tune.x_slabs == 0 &&
         footprint > kMallResident && (double)n * sv > 256.0 * 1024)
       want = irregular_gathers(rp, col, m, sv);
     if (want) {

@@ -120,10 +120,14 @@ class Info(C.Structure):
                 ("rccl_version", C.c_int32), ("reserved0", C.c_int32),
                 ("csort_chunks", C.c_int64), ("csort_seg_chunks", C.c_int64),
                 ("slab_kernel_rule", C.c_int32), ("lds_pad", C.c_int32),
-                ("heavy_group_frac", C.c_double)]
+                ("heavy_group_frac", C.c_double),
+                # since 1.1
+                ("csort_fixed_point", C.c_int32), ("reserved1", C.c_int32)]
 
 
 CSR3_PLANS = {"auto": 0, "aligned": 1, "packed": 2, "ssr": 3}
+# hspmv_options.deterministic (HSPMV_DETERMINISTIC_*)
+DETERMINISTIC = {"any": 0, "ordered": 1, "reproducible": 2}
 CSR3_PLAN_NAMES = {0: None, 1: "aligned", 2: "packed", 3: "ssr", 4: "row_groups"}
 
 
@@ -162,6 +166,8 @@ def make_options(flags: int, tuning: dict | None, *, device: int = 0, stream=Non
             raise ValueError(f"unknown hspmv option {k!r} (one of {', '.join(Options.TUNABLE)})")
         if k == "csr3_plan" and isinstance(v, str):
             v = CSR3_PLANS[v]
+        if k == "deterministic" and isinstance(v, str):
+            v = DETERMINISTIC[v]
         setattr(o, k, int(v))
     return o
 

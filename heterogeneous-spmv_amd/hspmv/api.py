@@ -321,7 +321,9 @@ class SpMV:
     device list (hspmv_create_sharded; devices may repeat); otherwise
     ``num_gpus`` GPUs with the row-range partition.  ``options``: explicit
     planner choices (hspmv_options fields by name, e.g. ``{"csr3_plan": "ssr",
-    "deterministic": 1}``; handle created with hspmv_create_ex).
+    "deterministic": "ordered"}`` -- deterministic 1 / "ordered": the ordered
+    row kernels; 2 / "reproducible": bit-identical run to run, csort with
+    fixed-point row sums allowed; handle created with hspmv_create_ex).
     """
 
     def __init__(self, A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, num_gpus: int = 1,

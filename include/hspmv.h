@@ -44,7 +44,10 @@ extern "C" {
  * Within a major, structs only grow at the end (hspmv_options.struct_size,
  * hspmv_get_info_sized) and signatures never change. */
 #define HSPMV_VERSION_MAJOR 1
-#define HSPMV_VERSION_MINOR 0
+#define HSPMV_VERSION_MINOR 1
+/* 1.1: hspmv_options.deterministic = 2 (HSPMV_DETERMINISTIC_REPRODUCIBLE),
+ * hspmv_info.csort_fixed_point; hspmv_get_info frozen at the 1.0 layout
+ * (HSPMV_INFO_SIZE_1_0). */
 
 /* ---------------------------------------------------------------- status */
 #define HSPMV_OK 0
@@ -160,10 +163,11 @@ typedef struct {
   double placement_us[8];   /* each set's mean SpMV time at creation, us    */
   /* since 0.2 */
   int32_t deterministic;    /* 1: y is bit-identical run to run (every kernel
-                               but CSORT, whose LDS row sums add in atomic
-                               order: fp32 y may differ in the last bit where
-                               an fp64 sum sits at an fp32 rounding tie, fp64
-                               y in the last bits of rows it sums)          */
+                               but CSORT with fp64 slots, whose LDS row sums
+                               add in atomic order: fp32 y may differ in the
+                               last bit where an fp64 sum sits at an fp32
+                               rounding tie, fp64 y in the last bits of rows
+                               it sums; CSORT with fixed-point slots is 1)  */
   int32_t csr3_plan;        /* CSR3 kernel: the HSPMV_CSR3_PLAN_* it runs;
                                0 for the other kernels                      */
   int32_t csort_slot_bytes; /* CSORT: LDS row-slot width (8 = fp64 sums)    */
@@ -189,6 +193,10 @@ typedef struct {
                                multiple of 16 LDS words long)              */
   double heavy_group_frac;  /* the share of nonzeros in heavy 64-row groups
                                the rule read (0 when it did not apply)     */
+  /* since 1.1 (hspmv_get_info_sized only) */
+  int32_t csort_fixed_point; /* CSORT: 1 = reproducible fixed-point row sums
+                                (hspmv_options.deterministic = 2)           */
+  int32_t reserved1;
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;
@@ -212,9 +220,11 @@ typedef struct hspmv_handle hspmv_handle;
                                   NOT bitwise vs omp_spmv and NOT bit-
                                   identical run to run: the sums add in
                                   LDS-atomic order (csort.hip,
-                                  hspmv_info.deterministic).  AUTO picks it
-                                  for HBM-resident matrices whose gathers
-                                  are irregular, unless
+                                  hspmv_info.deterministic) -- unless
+                                  hspmv_options.deterministic = 2, which
+                                  sums in fixed point (reproducible).  AUTO
+                                  picks it for HBM-resident matrices whose
+                                  gathers are irregular, unless
                                   hspmv_options.deterministic = 1          */
 #define HSPMV_KERNEL_MASK 0xFu
 /* lanes per row for VECTOR: HSPMV_LANES(L), L in {1,2,4,8,16,32,64}; 0=auto */
@@ -285,6 +295,8 @@ typedef struct hspmv_handle hspmv_handle;
 #define HSPMV_CSR3_PLAN_ROW_GROUPS 4 /* hspmv_info only: a CSR matrix (no
                                      maps) run by the CSR3 kernel over 64-row
                                      groups with the heavy ones cut         */
+#define HSPMV_DETERMINISTIC_ORDERED 1
+#define HSPMV_DETERMINISTIC_REPRODUCIBLE 2
 typedef struct {
   uint32_t struct_size;   /* sizeof(hspmv_options) of the caller            */
   uint32_t flags;         /* HSPMV_KERNEL_* | HSPMV_FLAG_* (hspmv_create)    */
@@ -305,10 +317,16 @@ typedef struct {
                              1, 2, 4                                        */
   int32_t csort_chunk_u;  /* csort entries per lane per chunk: 0, 4, 8, 16  */
   int32_t stream_waves;   /* STREAM waves per workgroup: 0 auto, 1, 2, 4    */
-  int32_t deterministic;  /* 1: never pick a kernel whose y bits depend on
-                             the hardware's scheduling (HSPMV_KERNEL_CSORT
-                             adds its row sums in LDS-atomic order); every
-                             other kernel gives the same bits on every run */
+  int32_t deterministic;  /* HSPMV_DETERMINISTIC_*: 0 the fastest kernel
+                             (CSORT's fp64 slot sums add in LDS-atomic
+                             order); 1 ORDERED: only the row kernels, which
+                             add each row in omp_spmv's order (bit-identical
+                             run to run, and to omp_spmv on rows of <= 40
+                             nonzeros); 2 REPRODUCIBLE: bit-identical run to
+                             run for a finite x -- CSORT then runs with
+                             fixed-point (int64) row sums: each product
+                             rounded once to 2^-50 of |its row's largest
+                             value| * |x|max (hspmv_info.csort_fixed_point) */
   int32_t placement_trials; /* array placements timed at creation (0/1
                                off, K <= 8; see hspmv_create_on_device)    */
 } hspmv_options;

@@ -108,11 +108,11 @@ def test_abi_major_is_in_the_soname():
     libhspmv.so.1 and its SONAME says so, so a binary linked against 0.x
     (NEEDED libhspmv.so) does not load it and misread arguments."""
     text = _lib.HEADER.read_text()
-    assert "#define HSPMV_VERSION_MAJOR 1" in text and "#define HSPMV_VERSION_MINOR 0" in text
+    assert "#define HSPMV_VERSION_MAJOR 1" in text and "#define HSPMV_VERSION_MINOR 1" in text
     assert _lib.LIB_PATH.name == "libhspmv.so.1"
     out = subprocess.run(["readelf", "-d", str(_lib.LIB_PATH)], capture_output=True, text=True)
     assert out.returncode == 0 and "Library soname: [libhspmv.so.1]" in out.stdout
-    assert hspmv.version().startswith("hspmv 1.0")
+    assert hspmv.version().startswith("hspmv 1.1")
     cli = _lib.PKG_ROOT / "build" / "spmv-csr"
     out = subprocess.run(["readelf", "-d", str(cli)], capture_output=True, text=True)
     assert "Shared library: [libhspmv.so.1]" in out.stdout

@@ -347,3 +347,161 @@ def test_csort_c5_shape_multi_shard():
     y = np.concatenate([run(A.rows(int(splits[r]), int(splits[r + 1])), x, kernel="csort")[0]
                         for r in range(2)])
     check(A, x, y)
+
+
+# ---------------------------------------------------------------- reproducible
+# hspmv_options.deterministic = 2 ("reproducible"): csort with fixed-point
+# (int64) LDS slots.  Each product v x is rounded once to an integer at the
+# scale 2^(50 - xexp - rexp[r]) -- |x| < 2^xexp, |v 2^rexp[r]| < 2^-extra
+# (extra > 0 only for a row kept whole beyond 4096 nonzeros) -- so y is the
+# same bits on every run, and differs from the exact sum by at most
+# len * 2^-49 * max_r|v| * max|x| * 2^extra (the rounding of the products)
+# plus the roundings of the partials and of y.
+
+def row_absmax(A):
+    a = np.abs(A.val.astype(np.float64))
+    lens = np.diff(A.row_ptr)
+    out = np.zeros(A.m)
+    nz = lens > 0
+    if a.size:
+        out[nz] = np.maximum.reduceat(a, A.row_ptr[:-1][nz])
+    return out
+
+
+def fixed_bound(A, x, split=True):
+    lens = np.diff(A.row_ptr).astype(np.float64)
+    extra = np.zeros_like(lens) if split else np.maximum(0, np.ceil(np.log2(np.maximum(lens, 1) / 4096)))
+    xmax = float(np.abs(x.astype(np.float64)).max()) if x.size else 0.0
+    return lens * 2.0 ** (-48 + extra) * row_absmax(A) * xmax
+
+
+def check_fixed(A, x, y, parts, split=True):
+    y64 = exact64(A, x)
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    err = np.abs(y.astype(np.float64) - y64)
+    fb = fixed_bound(A, x, split)
+    if A.val.dtype == np.float64:
+        tol = 2.0 ** -52 * (np.abs(y64) + (absrow if parts > 1 else 0.0)) + fb + 1e-300
+        assert np.all(err <= tol), float((err - tol).max())
+        assert fp64_tol_ok(y, y64, absrow)
+    else:
+        tol = fp32_bound(y64, absrow, parts) + fb
+        assert np.all(err <= tol), float((err - tol).max())
+        y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+        lens = np.diff(A.row_ptr)
+        e32 = np.abs(y.astype(np.float64) - y32.astype(np.float64))
+        assert np.all(e32 <= (lens + 2) * 2.0 ** -23 * absrow + 1e-30)
+    return y64
+
+
+REPRO = {"deterministic": "reproducible"}
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("parts", [1, 2])
+def test_csort_reproducible_fixed_point(dtype, parts):
+    """deterministic = 2: the column-sorted kernel with fixed-point slots --
+    reported as deterministic, y the same bits on every run (LDS atomics in
+    any order), within the fixed-point bound of the exact sum."""
+    for name, A in _matrices():
+        A = A.astype(dtype)
+        x = gen.rand_x(A.n, 17).astype(dtype)
+        with hspmv.SpMV(A, kernel="csort", options=dict(REPRO, csort_parts=parts)) as op:
+            info = op.info
+            assert info["kernel_name"] == "csort" and info["csort_fixed_point"] == 1, name
+            assert info["deterministic"] == 1, name
+            op.set_x(x)
+            ys = []
+            for _ in range(5):
+                op.spmv()
+                ys.append(op.get_y())
+        for y in ys[1:]:
+            assert np.array_equal(y.view(np.uint8), ys[0].view(np.uint8)), name
+        check_fixed(A, x, ys[0], info["csort_parts"])
+
+
+def test_csort_reproducible_auto_and_option_rules():
+    """AUTO with deterministic = 2 keeps the column-sorted kernel for
+    irregular gathers (fixed-point); deterministic = 1 keeps the row kernels
+    and refuses csort; out-of-range values are refused."""
+    A = gen.powerlaw(2_000_000, seed=12, dtype=np.float32)
+    x = gen.rand_x(A.n, 2).astype(np.float32)
+    with hspmv.SpMV(A, options=REPRO) as op:
+        assert op.info["kernel_name"] == "csort" and op.info["csort_fixed_point"] == 1
+        assert op.info["deterministic"] == 1
+        y = op(x)
+    check_fixed(A, x, y, 2)
+    with hspmv.SpMV(A) as op:  # the default: fp64 slots in atomic order
+        assert op.info["csort_fixed_point"] == 0 and op.info["deterministic"] == 0
+    with pytest.raises(hspmv.HspmvError):
+        hspmv.SpMV(A, kernel="csort", options={"deterministic": "ordered"})
+    with pytest.raises(hspmv.HspmvError):
+        hspmv.SpMV(A, options={"deterministic": 3})
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_csort_reproducible_scales(dtype):
+    """The fixed-point scale follows the data: x of magnitude 1e-30 (the
+    per-SpMV x exponent), rows whose values sit at 1e-20 and 1e+20 (the
+    per-row value exponents), an all-zero x (y exactly 0), and a new x on the
+    same handle."""
+    A = gen.powerlaw(60_000, seed=5, dtype=np.float64)
+    rows = np.repeat(np.arange(A.m), np.diff(A.row_ptr))
+    scale = np.where(rows % 3 == 0, 1e-20, np.where(rows % 3 == 1, 1e20, 1.0))
+    lim = 1e30 if dtype == np.float32 else 1e300
+    A = hspmv.CsrMatrix(A.m, A.n, A.row_ptr, A.col_idx, np.clip(A.val * scale, -lim, lim)).astype(dtype)
+    x = (gen.rand_x(A.n, 3) * 1e-30).astype(dtype)
+    with hspmv.SpMV(A, kernel="csort", options=REPRO) as op:
+        assert op.info["csort_fixed_point"] == 1
+        y = op(x)
+        check_fixed(A, x, y, op.info["csort_parts"])
+        assert np.all(op(np.zeros(A.n, dtype)) == 0)
+        x2 = gen.rand_x(A.n, 4).astype(dtype)
+        check_fixed(A, x2, op(x2), op.info["csort_parts"])
+
+
+def test_csort_reproducible_long_rows_whole_and_sliced():
+    A = _long_rows(seed=8)
+    x = gen.rand_x(A.n, 2)
+    y1, i1 = run(A, x, kernel="csort", options=REPRO)
+    assert i1["csort_fixed_point"] == 1 and i1["n_split_rows"] > 0
+    check_fixed(A, x, y1, i1["csort_parts"])
+    # rows kept whole beyond 4096 nonzeros: their scale leaves 2^extra headroom
+    y2, i2 = run(A, x, kernel="csort", split_rows=False, options=REPRO)
+    assert i2["n_split_rows"] == 0
+    check_fixed(A, x, y2, i2["csort_parts"], split=False)
+
+
+def test_csort_reproducible_nonfinite_x():
+    """An Inf in x: the fixed-point scale is undefined, so that SpMV adds in
+    fp64 slots (rows touching the Inf are Inf / NaN as omp_spmv gives them,
+    the others within the fp64 tolerance); the next finite x is fixed-point
+    again and bit-reproducible."""
+    A = gen.powerlaw(30_000, seed=6, dtype=np.float64)
+    x = gen.rand_x(A.n, 5)
+    c = int(A.col_idx[A.row_ptr[100]])
+    x[c] = np.inf
+    with hspmv.SpMV(A, kernel="csort", options=REPRO) as op:
+        y = op(x)
+        touched = np.zeros(A.m, bool)
+        rows = np.repeat(np.arange(A.m), np.diff(A.row_ptr))
+        touched[rows[A.col_idx == c]] = True
+        assert np.all(~np.isfinite(y[touched])) and np.all(np.isfinite(y[~touched]))
+        xs = x.copy()
+        xs[c] = 0.0
+        ys = exact64(A, xs)
+        absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, xs)
+        assert fp64_tol_ok(y[~touched], ys[~touched], absrow[~touched])
+        y1, y2 = op(xs), op(xs)
+        assert np.array_equal(y1.view(np.uint64), y2.view(np.uint64))
+        check_fixed(A, xs, y1, op.info["csort_parts"])
+
+
+def test_csort_reproducible_segmented_hub_rows():
+    A = _hub_rows().astype(np.float32)
+    x = gen.rand_x(A.n, 12).astype(np.float32)
+    with hspmv.SpMV(A, kernel="csort", options=dict(REPRO, csort_parts=2)) as op:
+        assert op.info["csort_seg_chunks"] > 0 and op.info["csort_fixed_point"] == 1
+        y1, y2 = op(x), op(x)
+    assert np.array_equal(y1.view(np.uint32), y2.view(np.uint32))
+    check_fixed(A, x, y1, 2)
