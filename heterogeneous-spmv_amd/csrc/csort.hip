@@ -161,16 +161,18 @@ __device__ __forceinline__ void load_entries(const void *__restrict__ ent, const
 }
 
 // Reproducible (fixed-point) slots, FIXP: each product v' x (v' = v 2^rexp,
-// scaled per row on the host so that |v'| < 1) is rounded ONCE to an integer
-// at scale 2^E, E = kCsortFixBits - xexp (|x| < 2^xexp): one fma with the
-// 1.5 * 2^52 rounding constant gives rint(v' x 2^E) in the low mantissa
-// bits, and the int64 difference of the bit patterns is that integer
-// (|q| < 2^50).  Integer adds are associative, so the slot's sum -- and y --
-// is the same bits whatever order the LDS atomics land in (ds_add_u64 costs
-// what ds_add_f64 does: profiles/r03/ab_c5_lds_add_ablation.jsonl).
-__device__ __forceinline__ long long fix_q(double v, double xs) {
-  const double r = __builtin_fma(v, xs, 0x1.8p52);
-  return (long long)(__builtin_bit_cast(unsigned long long, r) - 0x4338000000000000ull);
+// scaled per row on the host so that |v'| < 1) is rounded ONCE to a
+// multiple of 2^-E, E = kCsortFixBits - xexp (|x| < 2^xexp): with M = 1.5 *
+// 2^(52 - E) -- a per-SpMV constant -- fma(v', x, M) lands in M's binade,
+// whose ulp is 2^-E, so it IS M + rint(v' x 2^E) 2^-E, and the int64
+// difference of the bit patterns is that integer q (|q| < 2^50).  One fma
+// and a 64-bit subtraction per product, where the fp64-slot path has a mul.
+// Integer adds are associative, so the slot's sum -- and y -- is the same
+// bits whatever order the LDS atomics land in (ds_add_u64 costs what
+// ds_add_f64 does: profiles/r03/ab_c5_lds_add_ablation.jsonl).
+__device__ __forceinline__ long long fix_q(double v, double x, double M, unsigned long long mbits) {
+  const double r = __builtin_fma(v, x, M);
+  return (long long)(__builtin_bit_cast(unsigned long long, r) - mbits);
 }
 
 // The chunks of one workgroup (see hspmv_csort).  FIXP: integer slots (the
@@ -180,10 +182,11 @@ template <typename T, typename S, int U, bool NT, bool PF, bool WIDE, bool FIXP>
 __device__ __forceinline__ int32_t csort_chunks(int32_t c0, int32_t c1, int wid, int lane, int32_t dyn,
                                                 int32_t *next_chunk, const int32_t *__restrict__ cbase,
                                                 const void *__restrict__ ent, const T *__restrict__ val,
-                                                const T *__restrict__ x, void *slots, int32_t E) {
+                                                const T *__restrict__ x, void *slots, double M) {
   constexpr int NW = kCsortThreads / kWave;
   S *acc = reinterpret_cast<S *>(slots);
   unsigned long long *acq = reinterpret_cast<unsigned long long *>(slots);
+  const unsigned long long mbits = __builtin_bit_cast(unsigned long long, M);
   uint32_t ix[U];
   T vv[U];
 #if HSPMV_CSORT_ABL == 2 || HSPMV_CSORT_ABL == 3
@@ -236,7 +239,7 @@ __device__ __forceinline__ int32_t csort_chunks(int32_t c0, int32_t c1, int wid,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if constexpr (FIXP) {
-          const long long q = fix_q((double)vvc[u], __builtin_ldexp((double)xv[u], E));
+          const long long q = fix_q((double)vvc[u], (double)xv[u], M, mbits);
           atomicAdd(&acq[ixc[u] >> 16], (unsigned long long)q);
         } else {
           S pr;
@@ -281,7 +284,7 @@ __device__ __forceinline__ int32_t csort_chunks(int32_t c0, int32_t c1, int wid,
                              (start ? 1u : 0u);
         const bool last = lane == kWave - 1 || ((msk >> (lane + 1)) & 1ull);
         if constexpr (FIXP) {
-          unsigned long long q = (unsigned long long)fix_q((double)vvc[u], __builtin_ldexp((double)xv[u], E));
+          unsigned long long q = (unsigned long long)fix_q((double)vvc[u], (double)xv[u], M, mbits);
           q = seg_scan(q, rid);  // integer: the same sum in any association
           if (last) atomicAdd(&acq[sl], q);
         } else {
@@ -359,7 +362,9 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   int32_t xe = 0;
   if constexpr (FIX) xe = wave_xexp(xexp_part, n_xexp, lane);
   const bool fixp = FIX && xe != kCsortXexpNonFinite;  // uniform over the grid
-  const int32_t E = fixp ? kCsortFixBits - xe : 0;
+  // an x below 2^-1000 is scaled as if it reached 2^-1000 (M stays normal)
+  const int32_t E = fixp ? kCsortFixBits - max(xe, -1000) : 0;
+  const double M = fixp ? __builtin_ldexp(1.5, 52 - E) : 0.0;
   for (int32_t i = threadIdx.x; i <= nr + nv; i += kCsortThreads)  // + dummy; 0 = +0.0 = integer 0
     reinterpret_cast<S *>(smem)[i] = S(0);
   if (threadIdx.x == 0) next_chunk = c0 + NW;
@@ -368,10 +373,10 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   int32_t cn_done;
   if (fixp)
     cn_done = csort_chunks<T, S, U, NT, PF, WIDE, FIX>(c0, c1, wid, lane, dyn, &next_chunk, cbase, ent, val,
-                                                       x, smem, E);
+                                                       x, smem, M);
   else
     cn_done = csort_chunks<T, S, U, NT, PF, WIDE, false>(c0, c1, wid, lane, dyn, &next_chunk, cbase, ent,
-                                                         val, x, smem, 0);
+                                                         val, x, smem, 0.0);
   if (tr && lane == 0) {  // this wave's end and chunk count (its LDS adds issued)
     tr[4 + wid] = __builtin_amdgcn_s_memrealtime();
     tr[4 + NW + wid] = (unsigned long long)cn_done;
@@ -402,7 +407,8 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
 
 // Pre-pass of the fixed-point csort (one per SpMV, before it): per block the
 // max frexp exponent of |x| (|x| < 2^e), kCsortXexpNonFinite if the block saw
-// an Inf or a NaN; zeros do not count.  Every csort wave max-reduces the
+// an Inf or a NaN -- or an |x| >= 2^1020, whose rounding constant M would
+// overflow (that SpMV then adds in fp64 slots); zeros do not count.  Every csort wave max-reduces the
 // n_xexp block results itself (wave_xexp).
 template <typename T>
 __global__ __launch_bounds__(256) void hspmv_csort_xexp(int64_t n, const T *__restrict__ x,
@@ -411,7 +417,7 @@ __global__ __launch_bounds__(256) void hspmv_csort_xexp(int64_t n, const T *__re
   int32_t e = -0x40000000;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const double v = __builtin_fabs((double)x[i]);
-    if (!(v <= 1.7976931348623157e308)) e = kCsortXexpNonFinite;  // Inf, NaN
+    if (!(v < 0x1p1020)) e = kCsortXexpNonFinite;  // Inf, NaN, or beyond M's range
     else if (v != 0.0) e = max(e, __builtin_amdgcn_frexp_exp(v));
   }
 #pragma unroll

@@ -15,6 +15,7 @@
 #   rocprofleg[:ARGS]   the same with --marker-trace --kernel-rename: kernels
 #                       reported per bench leg (bench.py's roctx ranges)
 #   kstats:CFGS         tools/gpu_kstats.sh over run_one.py (CFGS comma separated)
+#   kstat1:NAME:ARGS    rocprofv3 --kernel-trace --stats over run_one.py ARGS (';' for spaces)
 #   pmc:CFG             tools/gpu_pmc_bench.sh TAG_CFG --config CFG (PMC traffic summary)
 #   ab:ARGS             tools/ab.py ARGS (commas inside ARGS: use ';' for spaces)
 #   py:NAME:SECS:ARGS   python ARGS (';' for spaces), log NAME, limit SECS
@@ -65,6 +66,14 @@ for step in "$@"; do
       grep '^{' $O/rocprof_leg.log > $O/bench_leg.json
       cp $O/prof_leg/*kernel_stats.csv $O/bench_leg_kernel_stats.csv 2>/dev/null
       head -12 $O/bench_leg_kernel_stats.csv | cut -c1-200 ;;
+    kstat1)
+      name=${arg%%:*}; rargs=${arg#*:}
+      echo "== kstat1 $name"
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d $O/prof_$name -o run -- python3 $R/$T/run_one.py ${rargs//;/ }) > $O/${name}_run.log 2>&1
+      rc=$?; echo "   rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/${name}_run.log; exit $rc; }
+      grep '^{' $O/${name}_run.log | cut -c1-300
+      cp $O/prof_$name/*kernel_stats.csv $O/${name}_kernel_stats.csv 2>/dev/null ;;
     kstats)
       run kstats 1200 bash $T/gpu_kstats.sh $TAG "${arg//,/ }" ;;
     pmc)

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--noxcd", action="store_true")
     ap.add_argument("--mi355x-maps", action="store_true")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--options", default="", help='hspmv_options as JSON, e.g. {"deterministic": 2}')
     ap.add_argument("--cold", type=int, default=0,
                     help="also time N launches each after a 512 MiB read (Infinity Cache evicted)")
     a = ap.parse_args()
@@ -40,7 +41,8 @@ def main():
     if a.kernel != "csr3" and a.kernel != "auto":
         maps = None
     op = hspmv.SpMV(A, maps, kernel=a.kernel, chunk_u=a.u, lanes=a.lanes, prefetch=a.pf,
-                    nontemporal=a.nt, xcd_remap=False if a.noxcd else None)
+                    nontemporal=a.nt, xcd_remap=False if a.noxcd else None,
+                    options=json.loads(a.options) if a.options else None)
     op.set_x(gen.rand_x(A.n, 42).astype(A.val.dtype))
     t = op.run(warmup=3, iters=a.iters)
     b = op.info["alg_bytes"]  # x counted as the distinct columns read

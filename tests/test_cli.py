@@ -194,3 +194,22 @@ def test_reference_pipeline_mtx_to_spmv(tmp_path):
         assert "Number Wrong: 0" in p.stdout and "Check: PASS" in p.stdout, (tool, f, p.stdout)
         harness_parse(p.stdout)
     assert hspmv.read_csr(rcm).nnz == A.nnz
+
+
+@pytest.mark.gpu
+def test_spmv_csr_reproducible_and_deterministic_flags(tmp_path):
+    """--reproducible (hspmv_options.deterministic = 2) runs the column-sorted
+    kernel with fixed-point sums: two runs dump the same y bits and the
+    serial check passes; --deterministic (1) refuses an explicit csort."""
+    f = GOLDEN / "powerlaw1500.csr"
+    ys = []
+    for i in range(2):
+        out = tmp_path / f"y{i}.bin"
+        p = run(BUILD / "spmv-csr", f, 5, "--kernel", "csort", "--reproducible", "--x", "rand:1",
+                "--dump-y", out)
+        assert "Kernel: csort" in p.stdout and "deterministic=1" in p.stdout
+        assert "Check: PASS" in p.stdout
+        ys.append(np.fromfile(out, np.float64))
+    assert np.array_equal(ys[0].view(np.uint64), ys[1].view(np.uint64))
+    p = run(BUILD / "spmv-csr", f, 3, "--kernel", "csort", "--deterministic", check=False)
+    assert p.returncode != 0

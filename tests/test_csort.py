@@ -52,7 +52,8 @@ def fp32_bound(y64, absrow, parts):
     column parts: fp32 row partials) one of each part's sum p_h, whose
     magnitudes add to at most sum|a x|; plus the fp64 summation error."""
     two = absrow if parts > 1 else 0.0
-    return 2.0 ** -24 * (np.abs(y64) + two) + 1e-12 * absrow
+    # (+ 2^-148: rounding into fp32's subnormal range is absolute, 2^-150 each)
+    return 2.0 ** -24 * (np.abs(y64) + two) + 1e-12 * absrow + 2.0 ** -148
 
 
 def check(A, x, y, parts=2):
