@@ -65,7 +65,6 @@ struct Tuning {
   int contig = 0;           // hipDeviceMallocContiguous allocations
   int xd_waves = 0;         // packed CSR3 tasks per dictionary block (0: 4; 8)
   int xd_blocks_per_cu = 0; // CSR3 dictionary blocks sized for this many per CU (0: 6; -1: no cuts)
-  int xd_persist = 0;       // CSR3 dictionary blocks run by persistent workgroups (hspmv_csr3_pers)
   double xslab_bytes = 0;   // x bytes per slab (0: 2 MiB)
   int csort_nt = -1, csort_pf = -1;      // -1: the library's choice
   int csort_blocks_per_cu = 0;           // row blocks per CU and part (0: 1)
@@ -206,7 +205,6 @@ struct LaunchPlan {
   int32_t groups = 1;      // STREAM: 64-row groups per wave (next group's rp prefetched)
   int32_t carry = 0;       // STREAM/CSR3: rows start from y (x-slab passes after the first)
   bool lds_pad = false;     // STREAM: bank-padded product buffers (spmv_device.cuh lds_ix)
-  bool persist = false;     // CSR3 + x dictionaries: persistent workgroups, next dictionary prefetched
   int64_t blocks = 0;
 };
 

@@ -99,7 +99,6 @@ void tuning_from_env(Tuning *t) {
   geti("HSPMV_CONTIG", &t->contig);
   geti("HSPMV_XD_WAVES", &t->xd_waves);
   geti("HSPMV_XD_BPC", &t->xd_blocks_per_cu);
-  geti("HSPMV_XD_PERSIST", &t->xd_persist);
   geti("HSPMV_PF", &t->pf);
   geti("HSPMV_YNT", &t->y_nt);
   geti("HSPMV_NT", &t->nt);

@@ -5,8 +5,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-
 #include "hspmv_internal.h"
 
 namespace hspmv {
@@ -700,116 +698,6 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
 #endif
 }
 
-// Persistent dictionary blocks (A/B, LaunchPlan.persist): a grid of as many
-// workgroups as the chip holds at once, workgroup g running blocks p = g, g +
-// G, g + 2G, ... (each remapped like blockIdx, so block p keeps its XCD).  The
-// NEXT block's dictionary is loaded into registers before this block's tasks
-// run -- its run records one block earlier still, so no round trip waits in
-// front of the tasks -- and written to the one LDS copy after a barrier:
-// the staging round trip overlaps the tasks instead of preceding them
-// (the r04 bpw attempt staged each block in turn).
-// KB entries per thread: 3072 fp64 / 6144 fp32 entries per dictionary at W = 4.
-template <typename T, int NTH>
-constexpr int pers_kb() {
-  return (sizeof(T) == 8 ? 3072 : 6144) / NTH;
-}
-
-// Lane-held run records of block blk (as stage_xdict reads them).
-__device__ __forceinline__ int2 xdict_records(const XDict &xd, int64_t blk, int lane, int32_t &r0, int32_t &nr) {
-  const int64_t rr = sload_i64(xd.blk, (uint64_t)blk * 4u);
-  r0 = (int32_t)rr;
-  nr = (int32_t)(rr >> 32) - r0 - 1;
-  int2 rec = make_int2(0, 0);
-  if (nr >= 0 && lane <= nr) rec = xd.runs[r0 + lane];
-  return rec;
-}
-
-// Issues the x loads of a block's dictionary into registers (entry j * NTH +
-// tid in v[j]); returns the entry count.
-template <typename T, int NTH, int KB>
-__device__ __forceinline__ int32_t xdict_load_regs(T (&v)[KB], const T *__restrict__ x, int2 rec, int32_t nr,
-                                                   int tid) {
-  const int32_t total = nr >= 0 ? __builtin_amdgcn_readlane(rec.y, nr) : 0;
-  const int32_t delta = rec.x - rec.y;
-  int32_t d[KB];
-#pragma unroll
-  for (int j = 0; j < KB; ++j) d[j] = 0;
-  for (int r = 0; r < nr; ++r) {
-    const int32_t o = __builtin_amdgcn_readlane(rec.y, r);
-    const int32_t dl = __builtin_amdgcn_readlane(delta, r);
-#pragma unroll
-    for (int j = 0; j < KB; ++j) d[j] = j * NTH + tid >= o ? dl : d[j];
-  }
-  const gchar *xb = uniform_ptr(x);
-#pragma unroll
-  for (int j = 0; j < KB; ++j) {
-    const int32_t e = min(j * NTH + tid, max(total - 1, 0));
-    v[j] = ld_off<false, T>(xb, (uint32_t)(e + d[j]) * (uint32_t)sizeof(T));
-  }
-  return total;
-}
-
-template <typename T, bool NT, int U, bool PF, int W>
-__global__ __launch_bounds__(W * 64) void hspmv_csr3_pers(
-    int32_t n_tasks, int32_t n_blocks, int32_t long_t, uint32_t xcd_chunk, int32_t y_nt, int32_t align,
-    const int32_t *__restrict__ task_start, XDict xd, const int32_t *__restrict__ rp, ColSrc cs,
-    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
-  constexpr int NTH = W * 64;
-  constexpr int KB = pers_kb<T, NTH>();
-  __shared__ T lds[W * wave_lds<U, false>()];
-  extern __shared__ __attribute__((aligned(16))) unsigned char xdyn[];  // the block's xs
-  T *xs = reinterpret_cast<T *>(xdyn);
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & (kWave - 1);
-  const uint32_t G = gridDim.x, nb = (uint32_t)n_blocks;
-  uint32_t p = blockIdx.x;
-  if (p >= nb) return;  // workgroup-uniform
-  int64_t blk = xcd_chunk_remap(p, nb, xcd_chunk);
-  stage_xdict<T, NTH>(xs, x, xd, blk, tid);  // the first block: staged in front
-  int32_t rn0 = 0, nrn = -1;
-  int2 recn = make_int2(0, 0);
-  if (p + G < nb) recn = xdict_records(xd, xcd_chunk_remap(p + G, nb, xcd_chunk), lane, rn0, nrn);
-  T *my = lds + wid * wave_lds<U, false>();
-  const XWin<T> win{xs, 0, 0};
-  while (true) {
-    const uint32_t pn = p + G;
-    const bool has_next = pn < nb;  // workgroup-uniform
-    // the next block's dictionary: its x loads now (records loaded one block
-    // ago), the records of the block after it too
-    T pre[KB];
-    int32_t total_n = 0;
-    if (has_next) total_n = xdict_load_regs<T, NTH, KB>(pre, x, recn, nrn, tid);
-    const uint32_t pnn = pn + G;
-    if (pnn < nb) recn = xdict_records(xd, xcd_chunk_remap(pnn, nb, xcd_chunk), lane, rn0, nrn);
-    // this block's W tasks from xs
-    const int64_t t = blk * W + wid;
-    if (t < n_tasks) {
-      const int64_t tb = sload_i64(task_start, (uint64_t)t * 4u);
-      const int32_t r0 = (int32_t)tb, r1 = (int32_t)(tb >> 32);
-      if (r0 < r1) {
-        const int32_t g1_first = min(align ? (r0 & ~(kWave - 1)) + kWave : r0 + kWave, r1);
-        int32_t beg, end;
-        group_bounds(rp, r0, g1_first, lane, beg, end);
-        for (int32_t g0 = r0, g1 = g1_first; g0 < r1; g0 = g1, g1 = min(g1 + kWave, r1)) {
-          int32_t nbeg = 0, nend = 0;
-          if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
-          wave_rows<T, NT, U, PF, 0, false, true, HSPMV_COOP_GROUPS != 0>(
-              g0, g1, beg, end, long_t, cs, val, x, y, my, lane, win, y_nt != 0, false, 0);
-          beg = nbeg;
-          end = nend;
-        }
-      }
-    }
-    __syncthreads();  // every wave is done with xs
-    if (!has_next) break;
-#pragma unroll
-    for (int j = 0; j < KB; ++j)
-      if (j * NTH + tid < total_n) xs[j * NTH + tid] = pre[j];
-    __syncthreads();
-    p = pn;
-    blk = xcd_chunk_remap(p, nb, xcd_chunk);
-  }
-}
-
 // ------------------------------------------------------------------ launchers
 
 inline ColSrc col_src(const DevCSR &A) {
@@ -864,24 +752,6 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
                      (int32_t)p.y_nt, p.carry, dp.task_align, dp.task_start, xw, xd, A.row_ptr, cs, \
                      val, x, y)
   if constexpr (XD) {  // packed tasks only (4 or 8 per block)
-    if constexpr (U == 4 || U == 16) {
-      // A/B (Tuning.xd_persist); every dictionary must fit the prefetch registers
-      if (p.persist && p.waves_per_block == 4 &&
-          (int64_t)dp.xd_lds_bytes <= (int64_t)pers_kb<T, 256>() * 256 * (int64_t)sizeof(T)) {
-        auto k = hspmv_csr3_pers<T, NT, U, PF, 4>;
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 256, dyn) != hipSuccess || per < 1)
-          return;
-        int64_t g = std::min<int64_t>(p.blocks, (int64_t)per * cus);
-        if (g >= kNumXcd) g -= g % kNumXcd;  // block p keeps its XCD (p % 8)
-        hipLaunchKernelGGL(k, dim3((unsigned)g), dim3(256), dyn, st, dp.n_tasks, (int32_t)p.blocks, dp.long_t,
-                           (uint32_t)p.xcd_chunk, (int32_t)p.y_nt, dp.task_align, dp.task_start, xd, A.row_ptr,
-                           cs, val, x, y);
-        return;
-      }
-    }
     if (p.waves_per_block == 8)
       HSPMV_CSR3(8, false, false, true);
     else

@@ -404,8 +404,6 @@ LaunchPlan plan_launch(const DevCSR &A, int dtype, unsigned flags, double rows_p
     if (t.lds_pad >= 0) p.lds_pad = can_pad && t.lds_pad > 0;
   }
   p.dyn_lds = t.dyn_lds;
-  p.persist = t.xd_persist > 0 && p.kernel == kCsr3 && A.has_xdict_tasks && p.waves_per_block == 4 &&
-              p.dyn_lds == 0;
   return p;
 }
 

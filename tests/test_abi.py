@@ -194,3 +194,29 @@ def test_get_info_null_output_and_canary():
         assert L.hspmv_get_info(h, ctypes.cast(buf, ctypes.POINTER(_lib.Info))) == 0
         assert all(buf[i] == 0xA5 for i in range(n10, len(buf)))
         assert bytes(buf[:n10]) == bytes(memoryview(full).cast("B")[:n10])
+
+
+def test_options_deterministic_values_are_validated_before_any_device():
+    """hspmv_options.deterministic: 0, 1 (ordered), 2 (reproducible); other
+    values, and an explicit column-sorted kernel with 1, are refused while
+    the options are read (HSPMV_E_INVALID), before any device is touched;
+    2 with the column-sorted kernel passes that check."""
+    import numpy as np
+    from hspmv import gen
+    L = hspmv.lib()
+    A = gen.laplace2d(8, 8)
+    cs = A.c_struct()
+    h = ctypes.c_void_p()
+    for det, kern, ok in ((3, 0, False), (-1, 0, False), (1, 4, False), (2, 4, True), (1, 0, True)):
+        o = _lib.make_options(kern, {"deterministic": det} if det >= 0 else None)
+        if det < 0:
+            o.deterministic = det
+        rc = L.hspmv_create_ex(ctypes.byref(h), ctypes.byref(cs), None, ctypes.byref(o))
+        if ok:
+            assert rc != -1 or b"deterministic" not in L.hspmv_last_error(), (det, kern)
+        else:
+            assert rc == -1, (det, kern)
+        if rc == 0:
+            L.hspmv_destroy(h)
+    assert _lib.make_options(0, {"deterministic": "reproducible"}).deterministic == 2
+    assert _lib.make_options(0, {"deterministic": "ordered"}).deterministic == 1
