@@ -319,10 +319,9 @@ __device__ __forceinline__ S slot_value(const void *slots, int32_t i, int32_t e)
 
 // The max exponent of |x| the workgroup's fixed-point scale comes from,
 // reduced by each wave from the pre-pass's per-block maxima.
-__device__ __forceinline__ int32_t wave_xexp(const int32_t *xexp_part, int32_t n, int lane) {
+__device__ __forceinline__ int32_t wave_xexp(const int32_t *__restrict__ xexp_part, int32_t n, int lane) {
   int32_t e = -0x40000000;
-  for (int32_t i = lane; i < n; i += kWave)  // agent scope: other workgroups wrote them (fused)
-    e = max(e, __hip_atomic_load(xexp_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (int32_t i = lane; i < n; i += kWave) e = max(e, xexp_part[i]);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) e = max(e, __shfl_xor(e, off, kWave));
   return __builtin_amdgcn_readfirstlane(e);
@@ -334,51 +333,6 @@ __device__ __forceinline__ int32_t xexp_max(int32_t e, double v) {
   v = __builtin_fabs(v);
   if (!(v < 0x1p1020)) return kCsortXexpNonFinite;
   return v != 0.0 ? max(e, __builtin_amdgcn_frexp_exp(v)) : e;
-}
-
-// Fused x exponent (DevCsort.fuse): workgroup b reduces its 1/G slice of x,
-// publishes it in xexp_part[b] and meets the grid at a sense-reversing
-// barrier (count, generation; the last arriver resets the count and bumps
-// the generation, so no host-side epoch is needed and a replayed launch
-// works too).  Only built when every workgroup of the grid is resident at
-// once (hspmv_csort_build.cpp); the spin is bounded all the same: a
-// workgroup that gives up returns false and adds in fp64 slots (correct,
-// not reproducible) instead of hanging.
-template <typename T>
-__device__ bool fused_xexp(const T *__restrict__ x, int64_t n_x, int32_t *xexp_part, unsigned *bar) {
-  __shared__ int32_t wmax[kCsortThreads / kWave];
-  __shared__ int32_t ok;
-  const int64_t G = gridDim.x, b = blockIdx.x;
-  int32_t e = -0x40000000;
-  for (int64_t i = n_x * b / G + threadIdx.x; i < n_x * (b + 1) / G; i += kCsortThreads)
-    e = xexp_max(e, (double)x[i]);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) e = max(e, __shfl_xor(e, off, kWave));
-  if ((threadIdx.x & (kWave - 1)) == 0) wmax[threadIdx.x >> 6] = e;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < kCsortThreads / kWave; ++w) e = max(e, wmax[w]);
-    const unsigned gen = __hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(xexp_part + b, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned c = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    int32_t done = 1;
-    if (c == (unsigned)G - 1u) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      int32_t spins = 0;
-      while (__hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1 << 22)) {  // ~0.1-1 s: give up (never expected)
-          done = 0;
-          break;
-        }
-      }
-    }
-    ok = done;
-  }
-  __syncthreads();
-  return ok != 0;
 }
 
 // S: the LDS row-slot / partial-sum type (double; float only for fp32 data,
@@ -393,7 +347,7 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
     const void *__restrict__ ent, const T *__restrict__ val, const T *__restrict__ x,
     P *__restrict__ part, S *__restrict__ spart, T *__restrict__ y,
     unsigned long long *__restrict__ trace, int32_t dyn, const int16_t *__restrict__ rexp,
-    const int16_t *__restrict__ sexp, int32_t *xexp_part, int32_t n_xexp, int64_t n_x, unsigned *bar) {
+    const int16_t *__restrict__ sexp, const int32_t *xexp_part, int32_t n_xexp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int32_t next_chunk;  // dyn: the workgroup's chunk queue head
   static_assert(!FIX || sizeof(S) == 8, "fixed-point slots are 8 bytes");
@@ -414,12 +368,8 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
   // FIX: the SpMV's x exponent (every wave reduces the pre-pass's maxima:
   // no LDS, no extra barrier); a non-finite x -> the S-slot fallback
   int32_t xe = 0;
-  bool met = true;
-  if constexpr (FIX) {
-    if (bar) met = fused_xexp(x, n_x, xexp_part, bar);  // fused: this launch computes the exponent
-    xe = wave_xexp(xexp_part, bar ? (int32_t)gridDim.x : n_xexp, lane);
-  }
-  const bool fixp = FIX && met && xe != kCsortXexpNonFinite;  // uniform over the grid
+  if constexpr (FIX) xe = wave_xexp(xexp_part, n_xexp, lane);
+  const bool fixp = FIX && xe != kCsortXexpNonFinite;  // uniform over the grid
   // an x below 2^-1000 is scaled as if it reached 2^-1000 (M stays normal)
   const int32_t E = fixp ? kCsortFixBits - max(xe, -1000) : 0;
   const double M = fixp ? __builtin_ldexp(1.5, 52 - E) : 0.0;
@@ -466,15 +416,36 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
 // Pre-pass of the fixed-point csort (one per SpMV, before it): per block the
 // max frexp exponent of |x| (|x| < 2^e), kCsortXexpNonFinite if the block saw
 // an Inf or a NaN -- or an |x| >= 2^1020, whose rounding constant M would
-// overflow (that SpMV then adds in fp64 slots); zeros do not count.  Every csort wave max-reduces the
+// overflow (that SpMV then adds in fp64 slots); zeros do not count.  Block j
+// takes chunks j, j + grid, ... of kXexpChunk entries, each thread 32 of a
+// chunk; VEC (x 16-byte aligned): all 32 in 16-byte loads issued before any
+// is used -- one memory round trip per chunk (a strided scalar loop ran
+// C5's 8 MB in 12.5 us, profiles/r06c).  Every csort wave max-reduces the
 // n_xexp block results itself (wave_xexp).
-template <typename T>
+constexpr int kXexpPerThread = 32;
+constexpr int64_t kXexpChunk = 256 * kXexpPerThread;
+
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void hspmv_csort_xexp(int64_t n, const T *__restrict__ x,
                                                         int32_t *__restrict__ out) {
   __shared__ int32_t wmax[4];
   int32_t e = -0x40000000;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    e = xexp_max(e, (double)x[i]);
+  for (int64_t c0 = (int64_t)blockIdx.x * kXexpChunk; c0 < n; c0 += (int64_t)gridDim.x * kXexpChunk) {
+    if (VEC && c0 + kXexpChunk <= n) {
+      constexpr int V = 16 / (int)sizeof(T), L = kXexpPerThread / V;
+      typedef T tv __attribute__((ext_vector_type(V)));
+      const tv *p = reinterpret_cast<const tv *>(x + c0) + threadIdx.x;
+      tv v[L];
+#pragma unroll
+      for (int j = 0; j < L; ++j) v[j] = p[j * 256];
+#pragma unroll
+      for (int j = 0; j < L; ++j)
+#pragma unroll
+        for (int k = 0; k < V; ++k) e = xexp_max(e, (double)v[j][k]);
+    } else {
+      for (int64_t i = c0 + threadIdx.x; i < min(n, c0 + kXexpChunk); i += 256) e = xexp_max(e, (double)x[i]);
+    }
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) e = max(e, __shfl_xor(e, off, kWave));
   if ((threadIdx.x & (kWave - 1)) == 0) wmax[threadIdx.x >> 6] = e;
@@ -553,21 +524,24 @@ template <typename T, typename S, typename P, int U, bool NT, bool PF, bool WIDE
 void launch_csort_main(const DevCsort &c, const T *x, P *part, S *spart, T *y, hipStream_t st) {
   if constexpr (sizeof(S) == 8) {
     if (c.fixed) {
-      if (!c.fuse)  // the x exponent by a pre-pass launch; fused: inside the csort launch
-        hipLaunchKernelGGL((hspmv_csort_xexp<T>), dim3((unsigned)c.n_xexp), dim3(256), 0, st, c.n_x, x,
+      const bool vec = reinterpret_cast<uintptr_t>(x) % 16 == 0;
+      if (vec)
+        hipLaunchKernelGGL((hspmv_csort_xexp<T, true>), dim3((unsigned)c.n_xexp), dim3(256), 0, st, c.n_x, x,
+                           c.xexp_part);
+      else
+        hipLaunchKernelGGL((hspmv_csort_xexp<T, false>), dim3((unsigned)c.n_xexp), dim3(256), 0, st, c.n_x, x,
                            c.xexp_part);
       hipLaunchKernelGGL((hspmv_csort<T, S, P, U, NT, PF, WIDE, true>), dim3((unsigned)c.n_wg),
                          dim3(kCsortThreads), (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r,
                          c.blk_v, c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y,
-                         c.trace, c.dyn ? 1 : 0, c.rexp, c.sexp, c.xexp_part, c.n_xexp, c.n_x,
-                         c.fuse ? c.bar : nullptr);
+                         c.trace, c.dyn ? 1 : 0, c.rexp, c.sexp, c.xexp_part, c.n_xexp);
       return;
     }
   }
   hipLaunchKernelGGL((hspmv_csort<T, S, P, U, NT, PF, WIDE, false>), dim3((unsigned)c.n_wg), dim3(kCsortThreads),
                      (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r, c.blk_v,
                      c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y,
-                     c.trace, c.dyn ? 1 : 0, nullptr, nullptr, nullptr, 0, 0, nullptr);
+                     c.trace, c.dyn ? 1 : 0, nullptr, nullptr, nullptr, 0);
 }
 
 template <typename T, typename S, typename P, int U, bool NT>
@@ -630,8 +604,7 @@ hipError_t launch_csort_nt(const DevCsort &c, const T *x, T *y, hipStream_t st) 
 hipError_t launch_csort(const DevCsort &c, int dtype, const void *x, void *y, hipStream_t st) {
   if (c.m == 0) return hipSuccess;
   if (c.n_wg <= 0 || c.lds_bytes > kCsortMaxLds) return hipErrorInvalidValue;
-  if (c.fixed && (c.slot32 || !c.rexp || !c.xexp_part || c.n_xexp <= 0 || c.n_xexp > kCsortXexpBlocks ||
-                  (c.fuse && !c.bar)))
+  if (c.fixed && (c.slot32 || !c.rexp || !c.xexp_part || c.n_xexp <= 0 || c.n_xexp > kCsortXexpBlocks))
     return hipErrorInvalidValue;
   if (dtype == 1) {
     if (c.slot32) return hipErrorInvalidValue;

@@ -589,18 +589,10 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
       return rc;
   }
   int32_t n_xexp = 0;
-  // Fused x exponent (csort.hip fused_xexp): a grid barrier inside the
-  // launch, so only when every workgroup is resident at once -- at most one
-  // per CU, which always fits (<= 160 KiB of LDS, 1024 threads).
-  const bool fuse = fixed && tn.csort_fix_fuse > 0 && G <= cus;
-  if (fixed) {
+  if (fixed) {  // the x-exponent pre-pass: one block per 8192 entries of x, at most kCsortXexpBlocks
     if ((rc = up(&s.d_cs_rexp, rexp)) || (rc = up(&s.d_cs_sexp, sexp))) return rc;
     n_xexp = (int32_t)std::min<int64_t>(kCsortXexpBlocks, std::max<int64_t>(1, (n + 256 * 32 - 1) / (256 * 32)));
-    if ((rc = dev_alloc(&s.d_cs_xexp, 4 * (size_t)std::max<int64_t>(n_xexp, G), &s.bytes))) return rc;
-    if (fuse) {
-      if ((rc = dev_alloc(&s.d_cs_bar, 2 * sizeof(unsigned), &s.bytes))) return rc;
-      HIP_TRY(hipMemset(s.d_cs_bar, 0, 2 * sizeof(unsigned)));
-    }
+    if ((rc = dev_alloc(&s.d_cs_xexp, 4 * (size_t)n_xexp, &s.bytes))) return rc;
   }
   // (An in-launch combine -- write-through partials, an arrival counter per
   // row block, the last arriver adding the parts -- measured slower than
@@ -626,8 +618,6 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   c.xexp_part = s.d_cs_xexp;
   c.n_xexp = n_xexp;
   c.n_x = n;
-  c.fuse = fuse;
-  c.bar = s.d_cs_bar;
   // waves claim chunks from the workgroup's LDS queue: one process, 7
   // rounds (profiles/r05c/ab_csort_dyn.jsonl): C5 106.9 -> 101.9 us median,
   // c5r 107.3 -> 104.9, fp64 C5 flat (175.7 -> 174.7)

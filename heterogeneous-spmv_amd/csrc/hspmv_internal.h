@@ -81,7 +81,6 @@ struct Tuning {
   double csort_sweep_w = 0;              // column-part cost of a column per row block (0: kSweepPerRowBlock)
   double csort_slack = 0;                // widest column part / (n / H) when balancing (0: kPartSlack)
   int csort_part32 = -1;                 // fp32 row partials over fp64 slots (fp32 data; -1: on, 0 off)
-  int csort_fix_fuse = -1;               // fixed-point csort: x exponent inside the launch (-1: default)
   int lds_pad = -1;                      // STREAM padded product buffers (-1: by row length, 0 off, 1 on)
   int pf = -1, y_nt = -1, nt = -1;       // row kernels: prefetch, nt y stores, nt col/val
   int dyn_lds = 0;
@@ -132,10 +131,8 @@ struct DevCsort {
   bool fixed = false;
   const int16_t *rexp = nullptr;  // per row: the exponent its values were scaled by (2^rexp)
   const int16_t *sexp = nullptr;  // per long-row slice: its row's rexp
-  int32_t *xexp_part = nullptr;   // per pre-pass block (fused: per workgroup): max frexp exponent of |x|
+  int32_t *xexp_part = nullptr;   // per pre-pass block: max frexp exponent of |x| (INT32_MAX: non-finite)
   int32_t n_xexp = 0;
-  bool fuse = false;              // the exponent found inside the csort launch (grid barrier)
-  unsigned *bar = nullptr;        // fused: the grid barrier's {count, generation}
   int64_t n_x = 0;                // x entries the pre-pass reads
   int32_t fin_rows = 0;   // rows per finishing-pass thread (0: 4, or the most m allows)
   int64_t m = 0;

@@ -72,7 +72,6 @@ struct Shard {
   double *d_cs_part = nullptr, *d_cs_spart = nullptr;
   int16_t *d_cs_rexp = nullptr, *d_cs_sexp = nullptr;  // reproducible csort: value scales
   int32_t *d_cs_xexp = nullptr;                        // reproducible csort: x exponent pre-pass
-  unsigned *d_cs_bar = nullptr;                        // reproducible csort, fused: grid barrier
   DevCsort csort;
   double csort_format_bytes = 0.0;   // bytes one csort SpMV moves
   int64_t csort_chunks = 0, csort_seg_chunks = 0;  // chunks, and those stored slot-sorted

@@ -57,7 +57,7 @@ void free_shard(Shard &s, bool borrowed) {
                   (void *)s.d_cs_vslice, (void *)s.d_cs_cbase, (void *)s.d_cs_long_row,
                   (void *)s.d_cs_long_cs, (void *)s.d_cs_mask, s.d_cs_ent, s.d_cs_val,
                   (void *)s.d_cs_part, (void *)s.d_cs_spart, (void *)s.d_cs_trace, (void *)s.d_cs_rexp,
-                  (void *)s.d_cs_sexp, (void *)s.d_cs_xexp, (void *)s.d_cs_bar})
+                  (void *)s.d_cs_sexp, (void *)s.d_cs_xexp})
     (void)hipFree(p);
   (void)hipFree(s.d_task);
   (void)hipFree(s.d_long_row);

@@ -506,3 +506,28 @@ def test_csort_reproducible_segmented_hub_rows():
         y1, y2 = op(x), op(x)
     assert np.array_equal(y1.view(np.uint32), y2.view(np.uint32))
     check_fixed(A, x, y1, 2)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_csort_reproducible_x_at_any_element_offset(dtype):
+    """The x-exponent pre-pass reads x with 16-byte loads when x is 16-byte
+    aligned and element by element otherwise (a caller's device x at any
+    element offset, hspmv_bind_x_device): both give the same exponent, so
+    the same y bits; an x length that is not a multiple of the pre-pass
+    chunk exercises its tail."""
+    import torch
+    A = gen.powerlaw(40_001, seed=4, dtype=dtype)
+    x = gen.rand_x(A.n, 6).astype(dtype)
+    tdt = torch.float32 if dtype == np.float32 else torch.float64
+    ys = []
+    with hspmv.SpMV(A, kernel="csort", options=REPRO) as op:
+        assert op.info["csort_fixed_point"] == 1
+        for off in (0, 1, 2, 3):
+            buf = torch.zeros(A.n + 8, dtype=tdt, device="cuda")
+            buf[off:off + A.n] = torch.from_numpy(x).to("cuda")
+            op.bind_x_device(buf.data_ptr() + off * buf.element_size())
+            op.spmv()
+            ys.append(op.get_y())
+    for y in ys[1:]:
+        assert np.array_equal(y.view(np.uint8), ys[0].view(np.uint8))
+    check_fixed(A, x, ys[0], 2)
