@@ -417,18 +417,22 @@ __global__ __launch_bounds__(kCsortThreads) void hspmv_csort(
 // max frexp exponent of |x| (|x| < 2^e), kCsortXexpNonFinite if the block saw
 // an Inf or a NaN -- or an |x| >= 2^1020, whose rounding constant M would
 // overflow (that SpMV then adds in fp64 slots); zeros do not count.  Block j
-// takes chunks j, j + grid, ... of kXexpChunk entries, each thread 32 of a
-// chunk; VEC (x 16-byte aligned): all 32 in 16-byte loads issued before any
-// is used -- one memory round trip per chunk (a strided scalar loop ran
-// C5's 8 MB in 12.5 us, profiles/r06c).  Every csort wave max-reduces the
-// n_xexp block results itself (wave_xexp).
-constexpr int kXexpPerThread = 32;
-constexpr int64_t kXexpChunk = 256 * kXexpPerThread;
+// takes chunks j, j + grid, ... of kXexpChunk entries, each of its 1024
+// threads 8 of a chunk; VEC (x 16-byte aligned): all 8 in 16-byte loads
+// issued before any is used -- one memory round trip per chunk, 16 waves
+// per CU in flight (a strided scalar loop of 256-thread blocks ran C5's 8 MB
+// in 12.5 us, profiles/r06c; 32 per thread of 256 still 5.7 us average,
+// r06d).  Every csort wave max-reduces the n_xexp block results itself
+// (wave_xexp).
+constexpr int kXexpThreads = 1024;
+constexpr int kXexpPerThread = 8;
+constexpr int64_t kXexpChunk = kXexpThreads * kXexpPerThread;
+static_assert(kXexpChunk == kCsortXexpChunk, "the host sizes the pre-pass grid by kCsortXexpChunk");
 
 template <typename T, bool VEC>
-__global__ __launch_bounds__(256) void hspmv_csort_xexp(int64_t n, const T *__restrict__ x,
-                                                        int32_t *__restrict__ out) {
-  __shared__ int32_t wmax[4];
+__global__ __launch_bounds__(kXexpThreads) void hspmv_csort_xexp(int64_t n, const T *__restrict__ x,
+                                                                 int32_t *__restrict__ out) {
+  __shared__ int32_t wmax[kXexpThreads / kWave];
   int32_t e = -0x40000000;
   for (int64_t c0 = (int64_t)blockIdx.x * kXexpChunk; c0 < n; c0 += (int64_t)gridDim.x * kXexpChunk) {
     if (VEC && c0 + kXexpChunk <= n) {
@@ -437,20 +441,26 @@ __global__ __launch_bounds__(256) void hspmv_csort_xexp(int64_t n, const T *__re
       const tv *p = reinterpret_cast<const tv *>(x + c0) + threadIdx.x;
       tv v[L];
 #pragma unroll
-      for (int j = 0; j < L; ++j) v[j] = p[j * 256];
+      for (int j = 0; j < L; ++j) v[j] = p[j * kXexpThreads];
 #pragma unroll
       for (int j = 0; j < L; ++j)
 #pragma unroll
         for (int k = 0; k < V; ++k) e = xexp_max(e, (double)v[j][k]);
     } else {
-      for (int64_t i = c0 + threadIdx.x; i < min(n, c0 + kXexpChunk); i += 256) e = xexp_max(e, (double)x[i]);
+      for (int64_t i = c0 + threadIdx.x; i < min(n, c0 + kXexpChunk); i += kXexpThreads)
+        e = xexp_max(e, (double)x[i]);
     }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) e = max(e, __shfl_xor(e, off, kWave));
   if ((threadIdx.x & (kWave - 1)) == 0) wmax[threadIdx.x >> 6] = e;
   __syncthreads();
-  if (threadIdx.x == 0) out[blockIdx.x] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+  if (threadIdx.x < kWave) {
+    e = threadIdx.x < kXexpThreads / kWave ? wmax[threadIdx.x] : -0x40000000;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) e = max(e, __shfl_xor(e, off, kWave));
+    if (threadIdx.x == 0) out[blockIdx.x] = e;
+  }
 }
 
 // y[r] = part[r] + part[m + r] + ... (parts in order), except long rows:
@@ -526,11 +536,11 @@ void launch_csort_main(const DevCsort &c, const T *x, P *part, S *spart, T *y, h
     if (c.fixed) {
       const bool vec = reinterpret_cast<uintptr_t>(x) % 16 == 0;
       if (vec)
-        hipLaunchKernelGGL((hspmv_csort_xexp<T, true>), dim3((unsigned)c.n_xexp), dim3(256), 0, st, c.n_x, x,
-                           c.xexp_part);
+        hipLaunchKernelGGL((hspmv_csort_xexp<T, true>), dim3((unsigned)c.n_xexp), dim3(kXexpThreads), 0, st,
+                           c.n_x, x, c.xexp_part);
       else
-        hipLaunchKernelGGL((hspmv_csort_xexp<T, false>), dim3((unsigned)c.n_xexp), dim3(256), 0, st, c.n_x, x,
-                           c.xexp_part);
+        hipLaunchKernelGGL((hspmv_csort_xexp<T, false>), dim3((unsigned)c.n_xexp), dim3(kXexpThreads), 0, st,
+                           c.n_x, x, c.xexp_part);
       hipLaunchKernelGGL((hspmv_csort<T, S, P, U, NT, PF, WIDE, true>), dim3((unsigned)c.n_wg),
                          dim3(kCsortThreads), (unsigned)c.lds_bytes, st, c.H, c.m, c.direct, c.blk_c, c.blk_r,
                          c.blk_v, c.vslice, c.cbase, c.ent, static_cast<const T *>(c.val), x, part, spart, y,

@@ -591,7 +591,8 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   int32_t n_xexp = 0;
   if (fixed) {  // the x-exponent pre-pass: one block per 8192 entries of x, at most kCsortXexpBlocks
     if ((rc = up(&s.d_cs_rexp, rexp)) || (rc = up(&s.d_cs_sexp, sexp))) return rc;
-    n_xexp = (int32_t)std::min<int64_t>(kCsortXexpBlocks, std::max<int64_t>(1, (n + 256 * 32 - 1) / (256 * 32)));
+    n_xexp = (int32_t)std::min<int64_t>(kCsortXexpBlocks,
+                                        std::max<int64_t>(1, (n + kCsortXexpChunk - 1) / kCsortXexpChunk));
     if ((rc = dev_alloc(&s.d_cs_xexp, 4 * (size_t)n_xexp, &s.bytes))) return rc;
   }
   // (An in-launch combine -- write-through partials, an arrival counter per

@@ -115,6 +115,7 @@ constexpr int kCsortTraceSlots = 4 + 2 * (kCsortThreads / 64);
 // workgroups at most.
 constexpr int kCsortFixBits = 50;
 constexpr int kCsortXexpBlocks = 256;
+constexpr int64_t kCsortXexpChunk = 8192;  // x entries per pre-pass block and chunk
 constexpr int32_t kCsortXexpNonFinite = 0x7fffffff;
 struct DevCsort {
   int32_t n_wg = 0, H = 1, u = 16, direct = 0, n_long = 0;

@@ -364,6 +364,42 @@ def test_config_c5_powerlaw_csr3_fp32():
     assert np.array_equal(ys[ok].view(np.uint32), y32[ok].view(np.uint32))
 
 
+@pytest.mark.parametrize("rcm", [False, True])
+def test_config_c5_reproducible_fixed_point(rcm):
+    """BASELINE configs[4] (and its RCM ordering) with hspmv_options
+    deterministic = 2: the column-sorted kernel with fixed-point (int64) row
+    sums.  Twelve back-to-back SpMVs give the same y bits; y stays within
+    omp_spmv's own fp32 summation error (the parity bar above) and within the
+    fixed-point bound of the exact sum (len 2^-49 max_r|v| max|x| + the
+    partials' and y's fp32 roundings)."""
+    A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32, rcm=rcm)
+    maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
+    x = gen.rand_x(A.n, 9).astype(np.float32)
+    lens = np.diff(A.row_ptr)
+    y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    y32 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    vmax = np.zeros(A.m)
+    nz = lens > 0
+    vmax[nz] = np.maximum.reduceat(np.abs(A.val.astype(np.float64)), A.row_ptr[:-1][nz])
+    fixed = lens * 2.0 ** -48 * vmax * float(np.abs(x).max())
+    with hspmv.SpMV(A, maps, device=0, options={"deterministic": "reproducible"}) as op:
+        info = op.info
+        assert info["kernel_name"] == "csort" and info["csort_fixed_point"] == 1
+        assert info["deterministic"] == 1
+        op.set_x(x)
+        ys = []
+        for _ in range(12):
+            op.spmv()
+            ys.append(op.get_y())
+    for y in ys[1:]:
+        assert np.array_equal(y.view(np.uint32), ys[0].view(np.uint32))
+    y = ys[0]
+    err = np.abs(y.astype(np.float64) - y32.astype(np.float64))
+    assert np.all(err <= (lens + 2) * 2.0 ** -23 * absrow + 1e-30)
+    assert np.all(np.abs(y - y64) <= 2.0 ** -24 * (np.abs(y64) + absrow) + fixed + 2.0 ** -148)
+
+
 def test_config_c5r_powerlaw_rcm_csr3_fp32():
     """C5's matrix in the reference's input ordering: RCM-permuted
     (helpers/converter.m:8,14, symrcm -> .mtx.rcm.csr).  RCM leaves a
