@@ -158,22 +158,29 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
   // 2^62.  A value that the scaling takes below the type's normal range loses
   // bits only below the products' rounding unit (2^-kCsortFixBits of the
   // row's largest).
-  const bool fixed = tn.deterministic == 2 && !slot32;
+  // A matrix with an Inf or NaN value has no fixed-point scale for its row
+  // (the product must stay non-finite): such a handle keeps fp64 slots and
+  // reports csort_fixed_point = 0, deterministic = 0.
+  bool fixed = tn.deterministic == 2 && !slot32;
   std::vector<int16_t> rexp(fixed ? (size_t)m : 0, 0), sexp;
   if (fixed) {
-    for (int64_t r = 0; r < m; ++r) {
+    for (int64_t r = 0; r < m && fixed; ++r) {
       double mx = 0.0;
       for (int32_t k = rp[r]; k < rp[r + 1]; ++k) {
         const double v = dtype == HSPMV_F32 ? (double)static_cast<const float *>(val)[k]
                                             : static_cast<const double *>(val)[k];
         mx = std::max(mx, std::fabs(v));
+        if (!std::isfinite(v)) fixed = false;
       }
-      if (!(mx > 0.0) || !std::isfinite(mx)) continue;  // empty / zero rows (non-finite values: as 2^0)
+      if (!(mx > 0.0) || !std::isfinite(mx)) continue;  // empty / zero rows
       const int64_t len = rp[r + 1] - rp[r];
       int extra = 0;  // (a sliced row's slots hold kCsortSlice <= 4096 products each)
       while (len <= long_t && ((int64_t)4096 << extra) < len) ++extra;
       rexp[(size_t)r] = (int16_t)(-(std::ilogb(mx) + 1) - extra);
     }
+    if (!fixed) std::vector<int16_t>().swap(rexp);
+  }
+  if (fixed) {
     sexp.resize((size_t)std::max<int64_t>(n_slices, 1), 0);
     for (size_t j = 0; j + 1 < lcs.size(); ++j)
       for (int32_t sl = lcs[j]; sl < lcs[j + 1]; ++sl) sexp[(size_t)sl] = rexp[(size_t)lrow[j]];

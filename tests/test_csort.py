@@ -531,3 +531,24 @@ def test_csort_reproducible_x_at_any_element_offset(dtype):
     for y in ys[1:]:
         assert np.array_equal(y.view(np.uint8), ys[0].view(np.uint8))
     check_fixed(A, x, ys[0], 2)
+
+
+def test_csort_reproducible_refused_for_nonfinite_matrix_values():
+    """A matrix value that is Inf or NaN has no fixed-point scale (its
+    products must stay non-finite): deterministic = 2 then keeps fp64 slots
+    and says so (csort_fixed_point = 0, deterministic = 0); the row holding
+    it is non-finite, as omp_spmv's, the others within the tolerance."""
+    A = gen.powerlaw(30_000, seed=8, dtype=np.float64)
+    val = A.val.copy()
+    val[A.row_ptr[77]] = np.inf
+    B = hspmv.CsrMatrix(A.m, A.n, A.row_ptr, A.col_idx, val)
+    x = gen.rand_x(B.n, 3)
+    with hspmv.SpMV(B, kernel="csort", options=REPRO) as op:
+        assert op.info["csort_fixed_point"] == 0 and op.info["deterministic"] == 0
+        y = op(x)
+    assert not np.isfinite(y[77])
+    ok = np.ones(B.m, bool)
+    ok[77] = False
+    y64 = exact64(A, x)
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    assert fp64_tol_ok(y[ok], y64[ok], absrow[ok])
