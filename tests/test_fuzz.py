@@ -6,7 +6,8 @@ empty rows, short rows (<= 40 nonzeros, the ordered-sum path), medium rows
 clustered columns, sorted or unsorted columns with duplicates, exact zeros,
 m and n from 1 up, fp32 or fp64.  Every case runs AUTO, STREAM, VECTOR (a
 random lane count), CSR3 with freshly built maps under the aligned / packed /
-ssr plans, csort (auto and 4 column parts), AUTO with deterministic = 1,
+ssr plans, csort (auto, 4 column parts, and reproducible fixed-point sums:
+bit-identical on a second launch), AUTO with deterministic = 1,
 STREAM with split rows kept whole, AUTO over 2 x slabs, and AUTO over three
 row-range shards, each twice (two x vectors through one handle: no state may
 leak from one launch into the next).
@@ -91,21 +92,36 @@ def runs(A, rng):
         yield "csr3-ssr", {"maps": maps, "kernel": "csr3", "options": {"csr3_plan": "ssr"}}
     yield "csort", {"kernel": "csort"}
     yield "csort-4parts", {"kernel": "csort", "options": {"csort_parts": 4}}
+    yield "csort-repro", {"kernel": "csort", "options": {"deterministic": "reproducible"}}
     yield "auto-det", {"options": {"deterministic": 1}}
     yield "stream-whole-rows", {"kernel": "stream", "split_rows": False}
     yield "auto-2slabs", {"options": {"x_slabs": 2}}
     yield "sharded-3", {"devices": [0, 0, 0]}  # row-range shards (one device, repeated)
 
 
-def check(A, x, y, ordered, what):
+def fixed_point_term(A, x):
+    """Reproducible csort: each product rounded once to 2^-50 of its row's
+    largest |value| times max|x| (tests/test_csort.py fixed_bound)."""
+    lens = np.diff(A.row_ptr)
+    vmax = np.zeros(A.m)
+    nz = lens > 0
+    if A.nnz:
+        vmax[nz] = np.maximum.reduceat(np.abs(A.val.astype(np.float64)), A.row_ptr[:-1][nz])
+    xmax = float(np.abs(x.astype(np.float64)).max()) if x.size else 0.0
+    return lens * 2.0 ** -48 * vmax * xmax
+
+
+def check(A, x, y, ordered, what, fixed=False):
     y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
     absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
     lens = np.diff(A.row_ptr)
+    fx = fixed_point_term(A, x) if fixed else 0.0
+    err = np.abs(y.astype(np.float64) - y64)
     if A.val.dtype == np.float64:
-        assert fp64_tol_ok(y, y64, absrow), (what, float(np.abs(y - y64).max()))
+        tol = 1e-6 * np.abs(y64) + 1e-12 * absrow + fx
+        assert np.all(err <= tol), (what, float(err.max()))
     else:
-        err = np.abs(y.astype(np.float64) - y64)
-        assert np.all(err <= (lens + 2) * 2.0 ** -23 * absrow + 1e-30), (what, float(err.max()))
+        assert np.all(err <= (lens + 2) * 2.0 ** -23 * absrow + fx + 1e-30), (what, float(err.max()))
     if ordered:  # omp_spmv's bits on the short rows
         yo = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
         short = lens <= SERIAL_MAX
@@ -127,9 +143,14 @@ def test_fuzz_every_kernel_matches_oracle(seed):
         op = hspmv.SpMV(A, maps, **kw)  # a forced kernel that cannot be built falls back
         with op:
             name = op.info["kernel_name"]
+            fixed = op.info["csort_fixed_point"] == 1
             for i, x in enumerate(xs):
                 y = op(x)
-                check(A, x, y, name in ("stream", "csr3"), (desc, label, name, i))
+                check(A, x, y, name in ("stream", "csr3"), (desc, label, name, i), fixed)
+                if fixed:  # reproducible: the same bits again
+                    assert np.array_equal(op(x).view(np.uint8), y.view(np.uint8)), (desc, label, i)
+        if label == "csort-repro" and name == "csort":
+            name = "csort-fixed" if fixed else name
         ran.append((label, name))
         SEEN.add(name)
     assert len(ran) >= 10, (desc, ran)
@@ -139,4 +160,4 @@ def test_fuzz_ran_every_kernel():
     """The forced kernels really ran somewhere in the cases above."""
     if len(SEEN) == 0:
         pytest.skip("run with the fuzz cases")
-    assert {"stream", "vector", "csr3", "csort"} <= SEEN, SEEN
+    assert {"stream", "vector", "csr3", "csort", "csort-fixed"} <= SEEN, SEEN
