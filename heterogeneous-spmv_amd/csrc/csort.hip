@@ -16,20 +16,26 @@
 // Row sums: one fp64 LDS slot per row of the block (plus one per long-row
 // slice and a dummy slot for padding), accumulated with ds_add_f64.  The
 // products are formed exactly as omp_spmv forms them for fp64 (v*x rounded),
-// and exactly (fp32 x fp32 in fp64) for fp32; the fp64 sums are rounded to
-// the value type once.  The order of the additions is the atomic order, so
-// unlike the STREAM/CSR3 kernels this path is NOT bitwise equal to omp_spmv:
-// fp32 results are more accurate than omp_spmv's fp32 running sum (and equal
-// run to run except where an fp64 sum sits within an fp64 rounding of an
-// fp32 tie), fp64 results agree with it to the fp64 rounding of the sum.
+// and exactly (fp32 x fp32 in fp64) for fp32.  Each column part's fp64 row
+// sums are stored as partials (fp32 for fp32 data: part32, the default) and
+// added in a fixed order, in fp64, by the finishing pass, which rounds y.
+// The order of the slot additions is the atomic order, so unlike the
+// STREAM/CSR3 kernels this path is NOT bitwise equal to omp_spmv: fp32
+// results are within an fp32 rounding of y and of each part's sum of the
+// exact sum (more accurate than omp_spmv's fp32 running sum), equal run to
+// run except where an fp64 sum sits within an fp64 rounding of an fp32 tie;
+// fp64 results agree with omp_spmv to the fp64 rounding of the sum.  FIX
+// (hspmv_options.deterministic = 2): int64 fixed-point slots instead (see
+// fix_q), the same bits on every run.
 //
 // Layout (built on the host, hspmv_csort_build.cpp build_csort): entries padded to
 // whole chunks of 64*U; per chunk a base column (cbase); per entry idx =
 // slot << 16 | (col - base) (a chunk never spans more than 65535 columns)
 // and the value: fp32 as one 8-byte {idx, val} record (one load per
-// element), fp64 as idx[] + val[].  The fp64 partial sums of the H parts
-// (part[h * m + row]) and of the long-row slices (spart[slice]) are combined
-// in a fixed order by hspmv_csort_finish.
+// element), fp64 as idx[] + val[] (FIX: the values scaled per row by
+// 2^rexp).  The partial sums of the H parts (part[h * m + row]) and of the
+// long-row slices (spart[slice], fp64) are combined in a fixed order by
+// hspmv_csort_finish.
 #include <hip/hip_runtime.h>
 
 #include "hspmv_internal.h"
