@@ -44,6 +44,8 @@ for f in $G/*.csr $D/powerlaw.csr $D/banded.csr $D/stencil.csr; do
   done
   step "csr_${b}_f32" $B/spmv-csr $f 3 --dtype f32 --x rand:1
   step "csr_${b}_det" $B/spmv-csr $f 3 --deterministic --x rand:1
+  step "csr_${b}_repro" $B/spmv-csr $f 3 --kernel csort --reproducible --x rand:1
+  step "csr_${b}_repro_f32" $B/spmv-csr $f 3 --kernel csort --reproducible --dtype f32 --x rand:1
 done
 for f in $G/*.csr3; do
   b=$(basename $f .csr3)
