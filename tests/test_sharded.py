@@ -87,6 +87,26 @@ def test_sharded_csort_and_fp32():
     assert np.array_equal(y[short].view(np.uint32), y32[short].view(np.uint32))
 
 
+def test_sharded_reproducible_csort():
+    """Row-range shards with deterministic = 2: every shard runs the
+    column-sorted kernel with fixed-point sums (each shard's pre-pass reads
+    the whole x, so every shard has the same scale); y is the same bits on
+    every run and within the fp64 bar plus the fixed-point term."""
+    A = gen.powerlaw(60_000, seed=9, dtype=np.float64)
+    x = gen.rand_x(A.n, 3)
+    with hspmv.SpMV(A, devices=[0, 0, 0], kernel="csort", options={"deterministic": "reproducible"}) as op:
+        assert op.info["kernel_name"] == "csort" and op.info["deterministic"] == 1
+        y1, y2 = op(x), op(x)
+    assert np.array_equal(y1.view(np.uint64), y2.view(np.uint64))
+    y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    lens = np.diff(A.row_ptr)
+    vmax = np.zeros(A.m)
+    vmax[lens > 0] = np.maximum.reduceat(np.abs(A.val), A.row_ptr[:-1][lens > 0])
+    fixed = lens * 2.0 ** -48 * vmax * np.abs(x).max()
+    assert np.all(np.abs(y1 - y64) <= 1e-6 * np.abs(y64) + 1e-12 * absrow + fixed)
+
+
 def test_sharded_rejects_bad_device_lists():
     A = gen.laplace2d(8, 8)
     for devices in ([], [-1], [0, 99]):
