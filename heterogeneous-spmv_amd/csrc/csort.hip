@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) void hspmv_csort_finish(
 #pragma unroll
         for (int j = 0; j < R; ++j) s[j] += (S)q[j];
       }
-      // R <= 8 rows never straddle a 32-row mask word (r is a multiple of R)
+      // R <= 4 rows never straddle a 32-row mask word (r is a multiple of R)
       const uint32_t lm = long_mask ? (long_mask[r >> 5] >> (r & 31)) & ((1u << R) - 1u) : 0u;
       if (lm == 0u) {
         tr o;
@@ -586,9 +586,9 @@ hipError_t launch_csort_p(const DevCsort &c, const T *x, T *y, hipStream_t st) {
   // c.fin_rows overrides (A/B)
   const int fr = c.fin_rows > 0 ? c.fin_rows : 4;
   const uintptr_t ya = reinterpret_cast<uintptr_t>(y);
-  if (fr >= 8 && c.m % 8 == 0 && ya % (8 * sizeof(T)) == 0)  // A/B (Tuning.csort_fin_rows = 8)
-    launch_finish<T, S, P, 8>(c, part, spart, y, st);
-  else if (fr >= 4 && c.m % 4 == 0 && ya % (4 * sizeof(T)) == 0)
+  // (8 rows per thread, 32-byte partial loads: C5 / c5r t_min +0.4 ... +2.6
+  // us against 4 in one process, profiles/r06l/ab_c5_fin_rows8_negative.jsonl)
+  if (fr >= 4 && c.m % 4 == 0 && ya % (4 * sizeof(T)) == 0)
     launch_finish<T, S, P, 4>(c, part, spart, y, st);
   else if (fr >= 2 && c.m % 2 == 0 && ya % (2 * sizeof(T)) == 0)
     launch_finish<T, S, P, 2>(c, part, spart, y, st);

@@ -76,7 +76,7 @@ struct Tuning {
   int csort_trace = 0;                   // per-workgroup timestamps (hspmv_diag_csort_trace)
   int csort_long = 0;                    // rows above this many nonzeros are sliced (0: kLongRow)
   int csort_balance = 0;                 // -1: equal-width column parts, nnz-balanced rows (r03)
-  int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4, 8)
+  int csort_fin_rows = 0;                // rows per finishing-pass thread (0: default; 1, 2, 4)
   int csort_dyn = -1;                    // chunks claimed from an LDS queue (-1: the library's choice)
   double csort_sweep_w = 0;              // column-part cost of a column per row block (0: kSweepPerRowBlock)
   double csort_slack = 0;                // widest column part / (n / H) when balancing (0: kPartSlack)
