@@ -552,3 +552,36 @@ def test_csort_reproducible_refused_for_nonfinite_matrix_values():
     y64 = exact64(A, x)
     absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
     assert fp64_tol_ok(y[ok], y64[ok], absrow[ok])
+
+
+@pytest.mark.parametrize("which", ["powerlaw60k", "hub_rows", "long_rows", "scaled"])
+def test_csort_reproducible_bitwise_vs_cpu_restatement(which):
+    """With one column part and fp32 data the fixed-point path's y is an
+    exact function of the inputs -- integer row sums, one conversion, one
+    scaling, one rounding -- restated on the CPU in tests/fixedpoint_model.py:
+    the GPU's y equals it bit for bit on every row the kernel does not slice
+    (rows of > 4096 nonzeros add their slices in the finishing pass's shuffle
+    tree; those are checked against the bound)."""
+    from fixedpoint_model import reproducible_csort_y
+    if which == "powerlaw60k":
+        A = gen.powerlaw(60_000, seed=5, dtype=np.float32)
+    elif which == "hub_rows":
+        A = _hub_rows().astype(np.float32)
+    elif which == "long_rows":
+        A = _long_rows(seed=8).astype(np.float32)
+    else:  # values and x across many binades
+        B = gen.powerlaw(60_000, seed=6, dtype=np.float64)
+        rows = np.repeat(np.arange(B.m), np.diff(B.row_ptr))
+        A = hspmv.CsrMatrix(B.m, B.n, B.row_ptr, B.col_idx,
+                            (B.val * 10.0 ** ((rows % 13) - 6)).astype(np.float32))
+    x = gen.rand_x(A.n, 31).astype(np.float32)
+    if which == "scaled":
+        x = (x * np.float32(1e-20)).astype(np.float32)
+    with hspmv.SpMV(A, kernel="csort", options=dict(REPRO, csort_parts=1)) as op:
+        assert op.info["csort_fixed_point"] == 1 and op.info["csort_parts"] == 1
+        y = op(x)
+    ym = reproducible_csort_y(A.row_ptr, A.col_idx, A.val, x)
+    short = np.diff(A.row_ptr) <= 4096
+    bad = np.flatnonzero(y[short].view(np.uint32) != ym[short].view(np.uint32))
+    assert bad.size == 0, (which, int(np.flatnonzero(short)[bad[0]]), y[short][bad[0]], ym[short][bad[0]])
+    check_fixed(A, x, y, 1)

@@ -107,3 +107,24 @@ def test_oracle_matches_live_reference_fp32(tmp_path):
         y = oracle.spmv(rp, ci, v32, x)
         assert np.array_equal(y.view(np.uint32), y_ref.view(np.uint32))
         assert np.array_equal(y_ser.view(np.uint32), y_ref.view(np.uint32))
+
+
+def test_fixedpoint_model_is_within_its_bound():
+    """tests/fixedpoint_model.py (the CPU restatement the reproducible csort
+    is checked against bitwise on the GPU): its y stays within the
+    fixed-point bound of the exact sum -- len 2^-49 max_r|v| max|x| plus an
+    fp32 rounding of y -- and is exactly 0 for x = 0."""
+    import numpy as np
+    from fixedpoint_model import reproducible_csort_y
+    from hspmv import gen
+    A = gen.powerlaw(20_000, seed=3, dtype=np.float32)
+    x = gen.rand_x(A.n, 5).astype(np.float32)
+    y = reproducible_csort_y(A.row_ptr, A.col_idx, A.val, x)
+    y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
+    lens = np.diff(A.row_ptr)
+    vmax = np.zeros(A.m)
+    vmax[lens > 0] = np.maximum.reduceat(np.abs(A.val.astype(np.float64)), A.row_ptr[:-1][lens > 0])
+    bound = lens * 2.0 ** -49 * vmax * np.abs(x).max() + 2.0 ** -24 * np.abs(y64) + 2.0 ** -148
+    ok = lens <= 4096
+    assert np.all(np.abs(y[ok].astype(np.float64) - y64[ok]) <= bound[ok])
+    assert np.all(reproducible_csort_y(A.row_ptr, A.col_idx, A.val, np.zeros(A.n, np.float32))[ok] == 0)
