@@ -433,6 +433,8 @@ static int fill_info(hspmv_handle *h, hspmv_info *out) {
   out->heavy_group_frac = s.heavy_frac < 0 ? 0.0 : s.heavy_frac;
   out->lds_pad = s.plan.lds_pad ? 1 : 0;
   out->csort_fixed_point = s.plan.kernel == kCsort && s.dp.cs.fixed ? 1 : 0;
+  if (s.plan.kernel == kCsort)
+    for (int hh = 0; hh < 4; ++hh) out->csort_part_begin[hh] = s.csort_part_begin[hh];
   for (auto &sh : h->shards)
     if (sh.plan.kernel == kCsort) {
       out->csort_chunks += sh.csort_chunks;

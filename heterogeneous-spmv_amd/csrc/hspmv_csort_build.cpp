@@ -645,6 +645,7 @@ int build_csort(Shard &s, const int32_t *rp, const int32_t *col, const void *val
     s.csort_wg_stats.swap(wst);
   }
   s.csort_chunks = tot_chunks;
+  for (int h = 0; h < 4; ++h) s.csort_part_begin[h] = h < H ? pb[(size_t)h] : 0;
   if (tn.csort_trace == 1 && (rc = dev_alloc(&s.d_cs_trace, 8 * kCsortTraceSlots * (size_t)G, &s.bytes))) return rc;
   c.trace = s.d_cs_trace;
   c.vslice = s.d_cs_vslice;

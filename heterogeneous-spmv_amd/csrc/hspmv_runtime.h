@@ -76,6 +76,7 @@ struct Shard {
   double csort_format_bytes = 0.0;   // bytes one csort SpMV moves
   int64_t csort_chunks = 0, csort_seg_chunks = 0;  // chunks, and those stored slot-sorted
   std::vector<int64_t> csort_wg_stats;  // diagnostic builds: 8 cost terms per workgroup
+  int64_t csort_part_begin[4] = {0, 0, 0, 0};  // first column of each column part
   int c16g_shape = 0;                // group-base columns built for kStream groups / kCsr3 tasks
   std::vector<int32_t> h_xwin;       // built at upload (host columns at hand)
   std::vector<int32_t> h_xwin_t;     // the same per packed CSR-3 task

@@ -122,7 +122,8 @@ class Info(C.Structure):
                 ("slab_kernel_rule", C.c_int32), ("lds_pad", C.c_int32),
                 ("heavy_group_frac", C.c_double),
                 # since 1.1
-                ("csort_fixed_point", C.c_int32), ("reserved1", C.c_int32)]
+                ("csort_fixed_point", C.c_int32), ("reserved1", C.c_int32),
+                ("csort_part_begin", C.c_int64 * 4)]
 
 
 CSR3_PLANS = {"auto": 0, "aligned": 1, "packed": 2, "ssr": 3}

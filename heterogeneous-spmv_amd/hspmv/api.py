@@ -454,6 +454,7 @@ class SpMV:
         check(lib().hspmv_get_info_sized(self._h, C.byref(i), C.sizeof(i)), "hspmv_get_info_sized")
         d = {k: getattr(i, k) for k, _ in _lib.Info._fields_}
         d["placement_us"] = [round(v, 3) for v in d["placement_us"][:d["placement_trials"]]]
+        d["csort_part_begin"] = [int(v) for v in d["csort_part_begin"][:max(d["csort_parts"], 0)]]
         d["kernel_name"] = KERNEL_NAMES.get(d["kernel"], "?")
         return d
 

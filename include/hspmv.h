@@ -46,7 +46,7 @@ extern "C" {
 #define HSPMV_VERSION_MAJOR 1
 #define HSPMV_VERSION_MINOR 1
 /* 1.1: hspmv_options.deterministic = 2 (HSPMV_DETERMINISTIC_REPRODUCIBLE),
- * hspmv_info.csort_fixed_point; hspmv_get_info frozen at the 1.0 layout
+ * hspmv_info.csort_fixed_point / csort_part_begin; hspmv_get_info frozen at the 1.0 layout
  * (HSPMV_INFO_SIZE_1_0). */
 
 /* ---------------------------------------------------------------- status */
@@ -197,6 +197,9 @@ typedef struct {
   int32_t csort_fixed_point; /* CSORT: 1 = reproducible fixed-point row sums
                                 (hspmv_options.deterministic = 2)           */
   int32_t reserved1;
+  int64_t csort_part_begin[4]; /* CSORT (GPU 0): first column of column part
+                                  h (h < csort_parts; part h ends where h + 1
+                                  begins, the last at n); 0 past the parts  */
 } hspmv_info;
 
 typedef struct hspmv_handle hspmv_handle;

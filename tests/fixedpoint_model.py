@@ -14,12 +14,12 @@ order in which the GPU adds them, so numpy can state it exactly:
 * y[r] = T(ldexp(double(sum_r q), -E - rexp[r])): the int64 sum converted to
   fp64 once (correctly rounded), scaled, rounded to the value type.
 
-This is what one column part (csort_parts = 1) gives for fp32 data on rows
-of <= 4096 nonzeros: the slot holds sum_r q, the workgroup writes the fp64
-value as the fp32 partial (or y directly), and the finishing pass adds one
-partial.  With two or more parts each part's sum is rounded on its own and
-the parts' boundaries come from the build's cost model, so those handles
-are checked against the error bound instead (tests/test_csort.py).
+This is what the kernel gives for fp32 data on rows of <= 4096 nonzeros:
+each column part's slot holds that part's sum_r q, the workgroup writes the
+fp64 value as an fp32 partial (or y directly with one part), and the
+finishing pass adds the partials in part order in fp64 and rounds y.  The
+parts' boundaries come from the build's cost model; the handle reports them
+(hspmv_info.csort_part_begin).
 """
 import numpy as np
 
@@ -47,10 +47,13 @@ def row_scales(row_ptr, val) -> np.ndarray:
     return rexp
 
 
-def reproducible_csort_y(row_ptr, col_idx, val, x) -> np.ndarray:
-    """y of the fixed-point csort with one column part, fp32 data (see the
-    module docstring); NaN on rows of more than 4096 nonzeros, which the
-    kernel slices (their slices add in the finishing pass's shuffle tree)."""
+def reproducible_csort_y(row_ptr, col_idx, val, x, part_begin=(0,)) -> np.ndarray:
+    """y of the fixed-point csort, fp32 data (see the module docstring);
+    NaN on rows of more than 4096 nonzeros, which the kernel slices (their
+    slices add in the finishing pass's shuffle tree).  part_begin: the first
+    column of each column part (hspmv_info.csort_part_begin): each part's
+    integer row sum becomes an fp64 value, rounded to an fp32 partial, and
+    the partials are added in part order in fp64 and rounded to y."""
     assert val.dtype == np.float32 and x.dtype == np.float32
     row_ptr = np.asarray(row_ptr, np.int64)
     lens = np.diff(row_ptr)
@@ -60,8 +63,15 @@ def reproducible_csort_y(row_ptr, col_idx, val, x) -> np.ndarray:
     vs = np.ldexp(val, rexp[rows].astype(np.int32))  # fp32, exact
     prod = vs.astype(np.float64) * x[col_idx].astype(np.float64)  # exact
     q = np.rint(np.ldexp(prod, E)).astype(np.int64)
-    s = np.zeros(lens.size, np.int64)
-    np.add.at(s, rows, q)
-    y = np.ldexp(s.astype(np.float64), (-E - rexp).astype(np.int32)).astype(np.float32)
+    bounds = np.asarray(list(part_begin), np.int64)
+    part = np.searchsorted(bounds, np.asarray(col_idx, np.int64), side="right") - 1
+    acc = np.zeros(lens.size, np.float64)
+    for h in range(bounds.size):
+        s = np.zeros(lens.size, np.int64)
+        sel = part == h
+        np.add.at(s, rows[sel], q[sel])
+        p = np.ldexp(s.astype(np.float64), (-E - rexp).astype(np.int32)).astype(np.float32)
+        acc = acc + p.astype(np.float64) if h else p.astype(np.float64)
+    y = acc.astype(np.float32)
     y[lens > 4096] = np.nan
     return y

@@ -554,14 +554,16 @@ def test_csort_reproducible_refused_for_nonfinite_matrix_values():
     assert fp64_tol_ok(y[ok], y64[ok], absrow[ok])
 
 
+@pytest.mark.parametrize("parts", [1, 2])
 @pytest.mark.parametrize("which", ["powerlaw60k", "hub_rows", "long_rows", "scaled"])
-def test_csort_reproducible_bitwise_vs_cpu_restatement(which):
-    """With one column part and fp32 data the fixed-point path's y is an
-    exact function of the inputs -- integer row sums, one conversion, one
-    scaling, one rounding -- restated on the CPU in tests/fixedpoint_model.py:
-    the GPU's y equals it bit for bit on every row the kernel does not slice
-    (rows of > 4096 nonzeros add their slices in the finishing pass's shuffle
-    tree; those are checked against the bound)."""
+def test_csort_reproducible_bitwise_vs_cpu_restatement(which, parts):
+    """With fp32 data the fixed-point path's y is an exact function of the
+    inputs and the column parts' boundaries -- integer row sums per part, one
+    conversion, one scaling and one rounding per part, the parts added in
+    order -- restated on the CPU in tests/fixedpoint_model.py: the GPU's y
+    equals it bit for bit on every row the kernel does not slice (rows of
+    > 4096 nonzeros add their slices in the finishing pass's shuffle tree;
+    those are checked against the bound)."""
     from fixedpoint_model import reproducible_csort_y
     if which == "powerlaw60k":
         A = gen.powerlaw(60_000, seed=5, dtype=np.float32)
@@ -577,11 +579,14 @@ def test_csort_reproducible_bitwise_vs_cpu_restatement(which):
     x = gen.rand_x(A.n, 31).astype(np.float32)
     if which == "scaled":
         x = (x * np.float32(1e-20)).astype(np.float32)
-    with hspmv.SpMV(A, kernel="csort", options=dict(REPRO, csort_parts=1)) as op:
-        assert op.info["csort_fixed_point"] == 1 and op.info["csort_parts"] == 1
+    with hspmv.SpMV(A, kernel="csort", options=dict(REPRO, csort_parts=parts)) as op:
+        info = op.info
+        assert info["csort_fixed_point"] == 1 and info["csort_parts"] == parts
+        pb = info["csort_part_begin"]
+        assert len(pb) == parts and pb[0] == 0 and all(a < b for a, b in zip(pb, pb[1:])) and pb[-1] < A.n
         y = op(x)
-    ym = reproducible_csort_y(A.row_ptr, A.col_idx, A.val, x)
+    ym = reproducible_csort_y(A.row_ptr, A.col_idx, A.val, x, pb)
     short = np.diff(A.row_ptr) <= 4096
     bad = np.flatnonzero(y[short].view(np.uint32) != ym[short].view(np.uint32))
     assert bad.size == 0, (which, int(np.flatnonzero(short)[bad[0]]), y[short][bad[0]], ym[short][bad[0]])
-    check_fixed(A, x, y, 1)
+    check_fixed(A, x, y, parts)

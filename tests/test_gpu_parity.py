@@ -398,6 +398,13 @@ def test_config_c5_reproducible_fixed_point(rcm):
     err = np.abs(y.astype(np.float64) - y32.astype(np.float64))
     assert np.all(err <= (lens + 2) * 2.0 ** -23 * absrow + 1e-30)
     assert np.all(np.abs(y - y64) <= 2.0 ** -24 * (np.abs(y64) + absrow) + fixed + 2.0 ** -148)
+    # and bit for bit the CPU restatement at the handle's own column parts
+    # (tests/fixedpoint_model.py) on every row the kernel does not slice
+    from fixedpoint_model import reproducible_csort_y
+    ym = reproducible_csort_y(A.row_ptr, A.col_idx, A.val, x, info["csort_part_begin"])
+    short = lens <= 4096
+    bad = np.flatnonzero(y[short].view(np.uint32) != ym[short].view(np.uint32))
+    assert bad.size == 0, (info["csort_part_begin"], int(np.flatnonzero(short)[bad[0]]))
 
 
 def test_config_c5r_powerlaw_rcm_csr3_fp32():
