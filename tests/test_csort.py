@@ -554,31 +554,33 @@ def test_csort_reproducible_refused_for_nonfinite_matrix_values():
     assert fp64_tol_ok(y[ok], y64[ok], absrow[ok])
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("parts", [1, 2])
 @pytest.mark.parametrize("which", ["powerlaw60k", "hub_rows", "long_rows", "scaled"])
-def test_csort_reproducible_bitwise_vs_cpu_restatement(which, parts):
-    """With fp32 data the fixed-point path's y is an exact function of the
-    inputs and the column parts' boundaries -- integer row sums per part, one
-    conversion, one scaling and one rounding per part, the parts added in
-    order -- restated on the CPU in tests/fixedpoint_model.py: the GPU's y
-    equals it bit for bit on every row the kernel does not slice (rows of
-    > 4096 nonzeros add their slices in the finishing pass's shuffle tree;
-    those are checked against the bound)."""
+def test_csort_reproducible_bitwise_vs_cpu_restatement(which, parts, dtype):
+    """The fixed-point path's y is an exact function of the inputs and the
+    column parts' boundaries -- one half-even rounding of each exact product,
+    integer row sums per part, one conversion, one scaling and one rounding
+    per part, the parts added in order -- restated on the CPU in
+    tests/fixedpoint_model.py (fp64 products exactly, in Python integers):
+    the GPU's y equals it bit for bit on every row the kernel does not slice
+    (rows of > 4096 nonzeros add their slices in the finishing pass's
+    shuffle tree; those are checked against the bound)."""
     from fixedpoint_model import reproducible_csort_y
     if which == "powerlaw60k":
-        A = gen.powerlaw(60_000, seed=5, dtype=np.float32)
+        A = gen.powerlaw(60_000, seed=5, dtype=dtype)
     elif which == "hub_rows":
-        A = _hub_rows().astype(np.float32)
+        A = _hub_rows().astype(dtype)
     elif which == "long_rows":
-        A = _long_rows(seed=8).astype(np.float32)
+        A = _long_rows(seed=8).astype(dtype)
     else:  # values and x across many binades
         B = gen.powerlaw(60_000, seed=6, dtype=np.float64)
         rows = np.repeat(np.arange(B.m), np.diff(B.row_ptr))
         A = hspmv.CsrMatrix(B.m, B.n, B.row_ptr, B.col_idx,
-                            (B.val * 10.0 ** ((rows % 13) - 6)).astype(np.float32))
-    x = gen.rand_x(A.n, 31).astype(np.float32)
+                            (B.val * 10.0 ** ((rows % 13) - 6)).astype(dtype))
+    x = gen.rand_x(A.n, 31).astype(dtype)
     if which == "scaled":
-        x = (x * np.float32(1e-20)).astype(np.float32)
+        x = (x * dtype(1e-20)).astype(dtype)
     with hspmv.SpMV(A, kernel="csort", options=dict(REPRO, csort_parts=parts)) as op:
         info = op.info
         assert info["csort_fixed_point"] == 1 and info["csort_parts"] == parts
@@ -587,6 +589,7 @@ def test_csort_reproducible_bitwise_vs_cpu_restatement(which, parts):
         y = op(x)
     ym = reproducible_csort_y(A.row_ptr, A.col_idx, A.val, x, pb)
     short = np.diff(A.row_ptr) <= 4096
-    bad = np.flatnonzero(y[short].view(np.uint32) != ym[short].view(np.uint32))
+    bad = np.flatnonzero(y[short] != ym[short])
     assert bad.size == 0, (which, int(np.flatnonzero(short)[bad[0]]), y[short][bad[0]], ym[short][bad[0]])
+    assert np.array_equal(y[short].view(np.uint8), ym[short].view(np.uint8))  # signed zeros too
     check_fixed(A, x, y, parts)

@@ -128,3 +128,23 @@ def test_fixedpoint_model_is_within_its_bound():
     ok = lens <= 4096
     assert np.all(np.abs(y[ok].astype(np.float64) - y64[ok]) <= bound[ok])
     assert np.all(reproducible_csort_y(A.row_ptr, A.col_idx, A.val, np.zeros(A.n, np.float32))[ok] == 0)
+
+
+def test_fixedpoint_model_fp64_is_within_its_bound():
+    """The fp64 branch of the model (exact products in Python integers,
+    fixedpoint_model.exact_q): within the fixed-point bound plus the fp64
+    roundings of the oracle's own sum."""
+    import numpy as np
+    from fixedpoint_model import reproducible_csort_y
+    from hspmv import gen
+    A = gen.powerlaw(8_000, seed=4, dtype=np.float64)
+    x = gen.rand_x(A.n, 6)
+    y = reproducible_csort_y(A.row_ptr, A.col_idx, A.val, x, (0, A.n // 3))
+    y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+    lens = np.diff(A.row_ptr)
+    vmax = np.zeros(A.m)
+    vmax[lens > 0] = np.maximum.reduceat(np.abs(A.val), A.row_ptr[:-1][lens > 0])
+    bound = lens * 2.0 ** -49 * vmax * np.abs(x).max() + (lens + 3) * 2.0 ** -53 * absrow + 1e-300
+    ok = lens <= 4096
+    assert np.all(np.abs(y[ok] - y64[ok]) <= bound[ok])
