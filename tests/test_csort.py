@@ -321,6 +321,33 @@ def test_csort_empty_and_degenerate():
         check(A, x, y)
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_csort_reproducible_empty_and_degenerate(dtype):
+    """test_csort_empty_and_degenerate's shapes (plus x = 0, whose scale
+    floors at 2^-1000) through the fixed-point path: the same bits twice,
+    and the CPU restatement's bits."""
+    from fixedpoint_model import reproducible_csort_y
+    cases = [(500, 1, np.ones(500, int), 1), (3, 7, np.array([0, 7, 0]), 1),
+             (2000, 3000, np.zeros(2000, int), 1), (4000, 5000, np.arange(4000) % 9, 0)]
+    for m, n, lens, xs in cases:
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        ci = np.concatenate([np.arange(ln) * 37 % n for ln in lens]).astype(np.int32) if rp[-1] else \
+            np.zeros(0, np.int32)
+        A = hspmv.CsrMatrix(m, n, rp, ci, np.linspace(-1, 1, rp[-1]).astype(dtype))
+        x = (gen.rand_x(n, 1) * xs).astype(dtype)
+        with hspmv.SpMV(A, kernel="csort", options=REPRO) as op:
+            info = op.info
+            y1, y2 = op(x), op(x)
+        assert np.array_equal(y1.view(np.uint8), y2.view(np.uint8)), (m, n)
+        if rp[-1] > 0:
+            assert info["kernel_name"] == "csort" and info["csort_fixed_point"] == 1, (m, n, info["kernel_name"])
+            pb = info["csort_part_begin"]
+            ym = reproducible_csort_y(A.row_ptr, A.col_idx, A.val, x, pb if pb else (0,))
+            assert np.array_equal(y1.view(np.uint8), ym.view(np.uint8)), (m, n)
+        else:
+            assert np.all(y1 == 0), (m, n, info["kernel_name"])
+
+
 def test_csort_auto_only_for_irregular_gathers():
     # banded / stencil matrices keep the ordered row kernels; a small random
     # matrix (cache-resident) too; csr3 maps do not stop the choice
