@@ -714,7 +714,8 @@ def test_full_size_fp32_bitwise_vs_reference_omp_spmv(cfg):
     into oracle/_ref): C2-C4 have no row over 32 nonzeros, so the GPU's y must
     be bit-identical everywhere (C3 through its CSR-3 maps); C5 (power-law,
     irregular gathers: the column-sorted kernel, fp64 row sums) within the
-    reference's fp32 summation error."""
+    reference's fp32 summation error, and with deterministic = 1 bitwise on
+    every row of <= SERIAL_MAX nonzeros."""
     if not oracle.ref_available():
         pytest.skip("oracle/_ref not built (no /root/reference where build() ran)")
     from hspmv import dist as hdist
@@ -744,6 +745,14 @@ def test_full_size_fp32_bitwise_vs_reference_omp_spmv(cfg):
     assert info["kernel_name"] == "csort"
     absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x.astype(np.float64))
     err = np.abs(y.astype(np.float64) - y_ref.astype(np.float64))
+    assert np.all(err <= (np.diff(A.row_ptr) + 2) * 2.0 ** -23 * absrow + 1e-30)
+    # deterministic = 1 (the ordered row kernels): omp_spmv's own fp32 sum,
+    # bit for bit, on every row the kernels add serially (<= SERIAL_MAX)
+    yd, idet = gpu_spmv(A, x, maps, options={"deterministic": 1})
+    assert idet["kernel_name"] != "csort" and idet["deterministic"] == 1
+    short = np.diff(A.row_ptr) <= SERIAL_MAX
+    assert np.array_equal(yd[short].view(np.uint32), y_ref[short].view(np.uint32))
+    err = np.abs(yd.astype(np.float64) - y_ref.astype(np.float64))
     assert np.all(err <= (np.diff(A.row_ptr) + 2) * 2.0 ** -23 * absrow + 1e-30)
 
 
