@@ -26,6 +26,9 @@
 //                       bit-identical run to run)
 //   --reproducible      y bit-identical run to run, the column-sorted kernel
 //                       allowed with fixed-point row sums
+//   --serial            every row summed in omp_spmv's order, one lane per
+//                       row: y bit-identical to the serial check (reported
+//                       as "Bitwise:")
 //   --dump-y PATH       write y as raw binary (dtype) for external checks
 //   --no-check          skip the serial CPU check
 #pragma once
@@ -109,6 +112,8 @@ inline bool parse_options(int argc, char **argv, int first, Options &o) {
       o.deterministic = HSPMV_DETERMINISTIC_ORDERED;
     } else if (a == "--reproducible") {
       o.deterministic = HSPMV_DETERMINISTIC_REPRODUCIBLE;
+    } else if (a == "--serial") {
+      o.deterministic = HSPMV_DETERMINISTIC_SERIAL;
     } else if (a == "--no-check") {
       o.check = false;
     } else if (a == "--dump-y") {
@@ -152,6 +157,7 @@ inline void fill_x(const Options &o, int64_t n, std::vector<double> &x64) {
 // (|diff| > 0.01) + relative-tolerance verdict.
 struct CheckResult {
   int wrong = 0;
+  int64_t bit_diff = 0;  // rows whose y is not bit-identical to the serial sum
   double maxrel = 0.0;
   bool pass = true;
 };
@@ -166,6 +172,7 @@ CheckResult check_y(const hspmv_csr_buf &A, const T *val, const T *x, const T *y
       temp += val[k] * x[A.col_idx[k]];
       mag += fabs((double)val[k] * (double)x[A.col_idx[k]]);
     }
+    if (memcmp(&y[row], &temp, sizeof(T)) != 0) r.bit_diff++;
     const double d = (double)y[row] - (double)temp;
     if (d > .01 || d < -.01) r.wrong++;
     const double tol_rel = sizeof(T) == 8 ? 1e-6 : 1e-4;
@@ -267,6 +274,10 @@ inline int run_and_report(const hspmv_csr_buf &A, const hspmv_csr3_buf *maps, in
     printf("Number Wrong: %d \n", r.wrong);
     printf("Check: %s maxrel=%.3e\n", r.pass ? "PASS" : "FAIL", r.maxrel);
     rc = r.pass ? 0 : 2;
+    if (o.deterministic == HSPMV_DETERMINISTIC_SERIAL) {  // the serial order's contract
+      printf("Bitwise: %lld rows differ\n", (long long)r.bit_diff);
+      if (r.bit_diff) rc = 2;
+    }
   }
   hspmv_destroy(h);
   return rc;

@@ -24,6 +24,7 @@ int check_handle(hspmv_handle *h) {
 int create_single(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps, int device,
                   void *stream, unsigned flags, const Tuning &tune) {
   ContigScope contig(tune);
+  if (int rc0 = apply_deterministic(&flags, tune)) return rc0;
   const bool devptrs = (flags & HSPMV_FLAG_DEVICE_PTRS) != 0;
   if (!A) return set_error(HSPMV_E_INVALID, "matrix is NULL");
   int ndev = 0;
@@ -433,6 +434,8 @@ static int fill_info(hspmv_handle *h, hspmv_info *out) {
   out->heavy_group_frac = s.heavy_frac < 0 ? 0.0 : s.heavy_frac;
   out->lds_pad = s.plan.lds_pad ? 1 : 0;
   out->csort_fixed_point = s.plan.kernel == kCsort && s.dp.cs.fixed ? 1 : 0;
+  out->serial_order = 1;
+  for (auto &sh : h->shards) out->serial_order &= sh.dp.serial_max == INT32_MAX ? 1 : 0;
   if (s.plan.kernel == kCsort)
     for (int hh = 0; hh < 4; ++hh) out->csort_part_begin[hh] = s.csort_part_begin[hh];
   for (auto &sh : h->shards)

@@ -95,6 +95,10 @@ enum Kernel : int { kAuto = 0, kVector = 1, kStream = 2, kCsr3 = 3, kCsort = 4 }
 // kLongChunk nonzeros, each summed by its own workgroup, and the chunk sums
 // are added per row by a second small kernel (deterministic order).
 constexpr int32_t kLongRow = 4096;
+// Rows of up to this many nonzeros are summed serially (omp_spmv's order) by
+// one lane in the row kernels; longer ones cooperatively (fixed DPP trees) --
+// unless DevPlan.serial_max raises the bound (deterministic = 3).
+constexpr int32_t kSerialMax = 40;
 constexpr int32_t kLongChunk = 4096;
 
 // Column-sorted row blocks (csort.hip): workgroup b works on column part
@@ -163,6 +167,7 @@ struct DevPlan {
   int32_t task_align = 0;
   // split rows
   int32_t long_t = 0x7fffffff;  // rows with more nonzeros are split rows
+  int32_t serial_max = kSerialMax;  // rows up to this length are summed serially
   int32_t n_long = 0, n_chunks = 0;
   const int32_t *long_row = nullptr;    // n_long row ids (shard-local)
   const int32_t *long_cstart = nullptr; // n_long+1, chunk ranges per split row

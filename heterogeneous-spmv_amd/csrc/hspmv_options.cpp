@@ -30,12 +30,12 @@ int tuning_from_options(const hspmv_options *o, Tuning *t) {
       (v.stream_waves && v.stream_waves != 1 && v.stream_waves != 2 && v.stream_waves != 4) ||
       v.task_nnz < 0 || v.x_dict_cap < 0 || v.placement_trials < 0 || v.placement_trials > 8)
     return set_error(HSPMV_E_INVALID, "hspmv_options: value out of range");
-  if (v.deterministic < 0 || v.deterministic > HSPMV_DETERMINISTIC_REPRODUCIBLE)
+  if (v.deterministic < 0 || v.deterministic > HSPMV_DETERMINISTIC_SERIAL)
     return set_error(HSPMV_E_INVALID, "deterministic %d unknown", v.deterministic);
-  if (v.deterministic == HSPMV_DETERMINISTIC_ORDERED && ((v.flags & 0xFu) == kCsort || v.csort > 0))
-    return set_error(HSPMV_E_INVALID, "the column-sorted kernel (HSPMV_KERNEL_CSORT, csort = 1) "
-                                      "does not sum in omp_spmv's order (deterministic = 2 runs it "
-                                      "with reproducible fixed-point sums)");
+  if ((v.deterministic == HSPMV_DETERMINISTIC_ORDERED || v.deterministic == HSPMV_DETERMINISTIC_SERIAL) &&
+      v.csort > 0)
+    return set_error(HSPMV_E_INVALID, "the column-sorted kernel (csort = 1) does not sum in omp_spmv's "
+                                      "order (deterministic = 2 runs it with reproducible fixed-point sums)");
   t->csr3_plan = v.csr3_plan;
   t->task_nnz = v.task_nnz;
   t->x_windows = v.x_windows < 0 ? -1 : 0;
@@ -107,6 +107,26 @@ void tuning_from_env(Tuning *t) {
 #else
 void tuning_from_env(Tuning *) {}
 #endif
+
+// The kernel rules of hspmv_options.deterministic 1 and 3 (checked at
+// creation, whatever set the mode): no CSORT (its sums do not follow
+// omp_spmv's order); SERIAL also no VECTOR (shuffle trees) and no split rows
+// (their pieces add in a second kernel) -- every row in one lane, in order.
+int apply_deterministic(unsigned *flags, const Tuning &t) {
+  const unsigned k = *flags & 0xFu;
+  if ((t.deterministic == HSPMV_DETERMINISTIC_ORDERED || t.deterministic == HSPMV_DETERMINISTIC_SERIAL) &&
+      k == kCsort)
+    return set_error(HSPMV_E_INVALID, "the column-sorted kernel (HSPMV_KERNEL_CSORT) does not sum in "
+                                      "omp_spmv's order (deterministic = 2 runs it with reproducible "
+                                      "fixed-point sums)");
+  if (t.deterministic == HSPMV_DETERMINISTIC_SERIAL) {
+    if (k == kVector)
+      return set_error(HSPMV_E_INVALID, "deterministic = 3 (serial order) runs the row kernels only: "
+                                        "HSPMV_KERNEL_VECTOR sums each row in a shuffle tree");
+    *flags |= HSPMV_FLAG_NO_SPLIT;
+  }
+  return HSPMV_OK;
+}
 
 Tuning default_tuning() {
   Tuning t;

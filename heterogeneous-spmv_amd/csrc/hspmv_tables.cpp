@@ -664,7 +664,7 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
   // the typical serially summed row (median length of the rows of 1..40
   // nonzeros, spmv_device.cuh kSerialMax): the planner's LDS bank rule
   {
-    constexpr int kSerial = 40;
+    constexpr int kSerial = kSerialMax;
     int64_t hist[kSerial + 1] = {0}, tot = 0;
     for (int64_t r = 0; r < m; ++r) {
       const int64_t len = rp[r + 1] - rp[r];
@@ -689,10 +689,10 @@ int build_row_tables(Shard &s, const int32_t *rp, const int32_t *col, const void
     const int cm = s.tune.csort;  // -1 off, 0 auto, 1 whenever it can be built
     const double sv = (double)dtype_size(dtype);
     const double footprint = (double)rp[m] * (sv + 4.0) + (double)m * (sv + 4.0) + (double)n * sv;
-    // an ordered handle (deterministic = 1) never builds the csort tables:
-    // the planner would pick kCsort whenever they exist (plan_launch); a
-    // reproducible one (2) builds them with fixed-point slots
-    const bool ordered = s.tune.deterministic == 1;
+    // an ordered or serial handle (deterministic = 1, 3) never builds the
+    // csort tables: the planner would pick kCsort whenever they exist
+    // (plan_launch); a reproducible one (2) builds them with fixed-point slots
+    const bool ordered = s.tune.deterministic == 1 || s.tune.deterministic == 3;
     bool want = !ordered && (kf == kCsort || cm == 1);
     // Scattered gathers from an x the L1 cannot hold go to the L2 one line
     // per nonzero, at its request rate, whatever the L2's capacity: until r04
@@ -747,6 +747,12 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
   const std::vector<int32_t> &rp = s.h_rp;
   const int64_t m = s.A.m;
   s.dp = DevPlan();
+  if (s.tune.deterministic == HSPMV_DETERMINISTIC_SERIAL) {  // every row by one lane, in order
+    if (s.plan.kernel != kStream && s.plan.kernel != kCsr3)
+      return set_error(HSPMV_E_INVALID, "deterministic = 3 (serial order) needs the row kernels, and "
+                                        "they cannot address this matrix (32-bit offsets)");
+    s.dp.serial_max = INT32_MAX;
+  }
   int64_t long_nnz = 0;
   if (s.plan.kernel == kCsort) {  // long rows are slices of the csort blocks
     s.dp.cs = s.csort;

@@ -66,10 +66,10 @@ constexpr int kWave = 64;
 #ifndef HSPMV_COOP_GROUPS
 #define HSPMV_COOP_GROUPS 1
 #endif
-#ifndef HSPMV_SERIAL_MAX
-#define HSPMV_SERIAL_MAX 40
-#endif
-constexpr int kSerialMax = HSPMV_SERIAL_MAX;  // longest row summed serially by one lane
+// kSerialMax (hspmv_internal.h): the longest row summed serially by one lane.
+// The kernels take the bound as an argument (DevPlan.serial_max): kSerialMax,
+// or INT32_MAX for hspmv_options.deterministic = 3, where every row is summed
+// serially -- omp_spmv's order for every row, the long ones by one lane.
 constexpr int kNumXcd = 8;
 
 // PAD: a wave's product buffer holds chunk position i at lds_ix(i) = i + i /
@@ -287,7 +287,7 @@ struct XWin {
 // stage B and C, so its latency overlaps the gather and the sums.
 template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD, bool GROUPS, bool PAD = false>
 __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, int32_t end,
-                                          int32_t long_t, const ColSrc &cs,
+                                          int32_t long_t, int32_t serial_max, const ColSrc &cs,
                                           const T *__restrict__ val,
                                           const T *__restrict__ x,
                                           T *__restrict__ y, T *lds, int lane,
@@ -300,8 +300,8 @@ __device__ __forceinline__ void wave_rows(int32_t g0, int32_t g1, int32_t beg, i
   (void)win;
   const bool skip = len > long_t;
   const unsigned long long skipmask = __ballot(valid && skip);
-  const unsigned long long coopmask = __ballot(valid && !skip && len > kSerialMax);
-  const bool serial = valid && !skip && len <= kSerialMax;
+  const unsigned long long coopmask = __ballot(valid && !skip && len > serial_max);
+  const bool serial = valid && !skip && len <= serial_max;
   const gchar *xb = uniform_ptr(x);
   const bool inwin = (XW && win.w > 0) || XD;
   // x slabs: passes after the first continue each row's sum from y, so a
@@ -566,7 +566,8 @@ __device__ __forceinline__ void stage_xdict(T *xs, const T *__restrict__ x, cons
 // kXWin entries gather from an LDS copy of it.
 template <typename T, bool NT, int U, bool PF, int C16, bool XW, bool XD, int W = 4, bool PAD = false>
 __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
-    int32_t m, int32_t long_t, uint32_t xcd_chunk, int32_t groups, int32_t y_nt, int32_t carry,
+    int32_t m, int32_t long_t, int32_t serial_max, uint32_t xcd_chunk, int32_t groups, int32_t y_nt,
+    int32_t carry,
     const int32_t *__restrict__ rp, ColSrc cs, const int2 *__restrict__ xwin, XDict xd,
     const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y) {
   static_assert(!XD || W == 4, "dictionaries are planned for 256-row blocks");
@@ -613,7 +614,8 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
     if (g1 < gend) group_bounds(rp, g1, (int32_t)min<int64_t>(g1 + kWave, gend), lane, nbeg, nend);
     int32_t gbase = 0;
     if constexpr (C16 == 2) gbase = (int32_t)sload_i64(cs.cbase, (uint64_t)(g0 / kWave) * 4u);
-    wave_rows<T, NT, U, PF, C16, XW, XD, false, PAD>((int32_t)g0, g1, beg, end, long_t, cs, val, x, y, my,
+    wave_rows<T, NT, U, PF, C16, XW, XD, false, PAD>((int32_t)g0, g1, beg, end, long_t, serial_max, cs, val,
+                                                     x, y, my,
                                          lane, win, y_nt != 0, carry != 0, gbase, ts);
     ts = nullptr;  // trace the first group only
     if (g1 >= gend) break;
@@ -625,7 +627,8 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr_stream(
 
 template <typename T, bool NT, int U, bool PF, int C16, int W, bool XW, bool XD>
 __global__ __launch_bounds__(W * 64) void hspmv_csr3(
-    int32_t n_tasks, int32_t long_t, uint32_t xcd_chunk, int32_t y_nt, int32_t carry, int32_t align,
+    int32_t n_tasks, int32_t long_t, int32_t serial_max, uint32_t xcd_chunk, int32_t y_nt, int32_t carry,
+    int32_t align,
     const int32_t *__restrict__ task_start, const int2 *__restrict__ xwin, XDict xd,
     const int32_t *__restrict__ rp, ColSrc cs, const T *__restrict__ val,
     const T *__restrict__ x, T *__restrict__ y) {
@@ -687,7 +690,8 @@ __global__ __launch_bounds__(W * 64) void hspmv_csr3(
   for (int32_t g0 = r0, g1 = g1_first; g0 < r1; g0 = g1, g1 = min(g1 + kWave, r1)) {
     int32_t nbeg = 0, nend = 0;
     if (g1 < r1) group_bounds(rp, g1, min(g1 + kWave, r1), lane, nbeg, nend);
-    wave_rows<T, NT, U, PF, C16, XW, XD, HSPMV_COOP_GROUPS != 0>(g0, g1, beg, end, long_t, cs, val, x, y, my, lane,
+    wave_rows<T, NT, U, PF, C16, XW, XD, HSPMV_COOP_GROUPS != 0>(g0, g1, beg, end, long_t, serial_max, cs, val,
+                                                                 x, y, my, lane,
                                          win, y_nt != 0, carry != 0, gbase, ts);
     ts = nullptr;
     beg = nbeg;
@@ -716,7 +720,8 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
     const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
 #define HSPMV_STREAM(C, XW, XDX, W, PAD)                                                            \
   hipLaunchKernelGGL((hspmv_csr_stream<T, NT, U, PF, C, XW, XDX, W, PAD>), dim3((unsigned)p.blocks), \
-                     dim3(W * 64), dyn, st, A.m, dp.long_t, (uint32_t)p.xcd_chunk, (int32_t)p.groups,  \
+                     dim3(W * 64), dyn, st, A.m, dp.long_t, dp.serial_max, (uint32_t)p.xcd_chunk,       \
+                     (int32_t)p.groups,                                                               \
                      (int32_t)p.y_nt, p.carry, A.row_ptr, cs, xw, xd, val, x, y)
     if constexpr (XD) {  // never padded (plan_launch: dictionaries are sized unpadded)
       HSPMV_STREAM(false, false, true, 4, false);
@@ -748,7 +753,8 @@ void launch_rows_u(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p, cons
   const int2 *xw = reinterpret_cast<const int2 *>(dp.xwin);
 #define HSPMV_CSR3(W, C, XW, X)                                                               \
   hipLaunchKernelGGL((hspmv_csr3<T, NT, U, PF, C, W, XW, X>), dim3((unsigned)p.blocks),      \
-                     dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, (uint32_t)p.xcd_chunk,     \
+                     dim3(W * 64), dyn, st, dp.n_tasks, dp.long_t, dp.serial_max,             \
+                     (uint32_t)p.xcd_chunk,                                                   \
                      (int32_t)p.y_nt, p.carry, dp.task_align, dp.task_start, xw, xd, A.row_ptr, cs, \
                      val, x, y)
   if constexpr (XD) {  // packed tasks only (4 or 8 per block)

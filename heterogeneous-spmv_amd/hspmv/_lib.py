@@ -122,13 +122,13 @@ class Info(C.Structure):
                 ("slab_kernel_rule", C.c_int32), ("lds_pad", C.c_int32),
                 ("heavy_group_frac", C.c_double),
                 # since 1.1
-                ("csort_fixed_point", C.c_int32), ("reserved1", C.c_int32),
+                ("csort_fixed_point", C.c_int32), ("serial_order", C.c_int32),
                 ("csort_part_begin", C.c_int64 * 4)]
 
 
 CSR3_PLANS = {"auto": 0, "aligned": 1, "packed": 2, "ssr": 3}
 # hspmv_options.deterministic (HSPMV_DETERMINISTIC_*)
-DETERMINISTIC = {"any": 0, "ordered": 1, "reproducible": 2}
+DETERMINISTIC = {"any": 0, "ordered": 1, "reproducible": 2, "serial": 3}
 CSR3_PLAN_NAMES = {0: None, 1: "aligned", 2: "packed", 3: "ssr", 4: "row_groups"}
 
 

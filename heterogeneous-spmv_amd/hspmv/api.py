@@ -323,7 +323,9 @@ class SpMV:
     planner choices (hspmv_options fields by name, e.g. ``{"csr3_plan": "ssr",
     "deterministic": "ordered"}`` -- deterministic 1 / "ordered": the ordered
     row kernels; 2 / "reproducible": bit-identical run to run, csort with
-    fixed-point row sums allowed; handle created with hspmv_create_ex).
+    fixed-point row sums allowed; 3 / "serial": every row summed in
+    omp_spmv's order, y bit-identical to it; handle created with
+    hspmv_create_ex).
     """
 
     def __init__(self, A: CsrMatrix, maps: Optional[Csr3Maps] = None, *, num_gpus: int = 1,

@@ -45,8 +45,9 @@ extern "C" {
  * hspmv_get_info_sized) and signatures never change. */
 #define HSPMV_VERSION_MAJOR 1
 #define HSPMV_VERSION_MINOR 1
-/* 1.1: hspmv_options.deterministic = 2 (HSPMV_DETERMINISTIC_REPRODUCIBLE),
- * hspmv_info.csort_fixed_point / csort_part_begin; hspmv_get_info frozen at the 1.0 layout
+/* 1.1: hspmv_options.deterministic = 2 (HSPMV_DETERMINISTIC_REPRODUCIBLE)
+ * and 3 (HSPMV_DETERMINISTIC_SERIAL), hspmv_info.csort_fixed_point /
+ * serial_order / csort_part_begin; hspmv_get_info frozen at the 1.0 layout
  * (HSPMV_INFO_SIZE_1_0). */
 
 /* ---------------------------------------------------------------- status */
@@ -196,7 +197,9 @@ typedef struct {
   /* since 1.1 (hspmv_get_info_sized only) */
   int32_t csort_fixed_point; /* CSORT: 1 = reproducible fixed-point row sums
                                 (hspmv_options.deterministic = 2)           */
-  int32_t reserved1;
+  int32_t serial_order;     /* 1: every row is summed in omp_spmv's order
+                                (hspmv_options.deterministic = 3): y is bit-
+                                identical to spmv-csr/spmv.c:92-114's loop  */
   int64_t csort_part_begin[4]; /* CSORT (GPU 0): first column of column part
                                   h (h < csort_parts; part h ends where h + 1
                                   begins, the last at n); 0 past the parts  */
@@ -300,6 +303,7 @@ typedef struct hspmv_handle hspmv_handle;
                                      groups with the heavy ones cut         */
 #define HSPMV_DETERMINISTIC_ORDERED 1
 #define HSPMV_DETERMINISTIC_REPRODUCIBLE 2
+#define HSPMV_DETERMINISTIC_SERIAL 3
 typedef struct {
   uint32_t struct_size;   /* sizeof(hspmv_options) of the caller            */
   uint32_t flags;         /* HSPMV_KERNEL_* | HSPMV_FLAG_* (hspmv_create)    */
@@ -322,14 +326,22 @@ typedef struct {
   int32_t stream_waves;   /* STREAM waves per workgroup: 0 auto, 1, 2, 4    */
   int32_t deterministic;  /* HSPMV_DETERMINISTIC_*: 0 the fastest kernel
                              (CSORT's fp64 slot sums add in LDS-atomic
-                             order); 1 ORDERED: only the row kernels, which
-                             add each row in omp_spmv's order (bit-identical
-                             run to run, and to omp_spmv on rows of <= 40
-                             nonzeros); 2 REPRODUCIBLE: bit-identical run to
+                             order); 1 ORDERED: only the row kernels (bit-
+                             identical run to run; rows of <= 40 nonzeros
+                             added in omp_spmv's order, longer ones in fixed
+                             trees); 2 REPRODUCIBLE: bit-identical run to
                              run for a finite x -- CSORT then runs with
                              fixed-point (int64) row sums: each product
                              rounded once to 2^-50 of |its row's largest
-                             value| * |x|max (hspmv_info.csort_fixed_point) */
+                             value| * |x|max (hspmv_info.csort_fixed_point);
+                             3 SERIAL: the row kernels add EVERY row left to
+                             right from 0, one lane per row, as omp_spmv
+                             does (spmv-csr/spmv.c:92-114): y bit-identical
+                             to it for every input, at the cost of long rows
+                             summed by one lane (implies HSPMV_FLAG_NO_SPLIT;
+                             VECTOR and CSORT refused; a matrix the row
+                             kernels cannot address fails with
+                             HSPMV_E_INVALID; hspmv_info.serial_order)      */
   int32_t placement_trials; /* array placements timed at creation (0/1
                                off, K <= 8; see hspmv_create_on_device)    */
 } hspmv_options;

@@ -197,17 +197,18 @@ def test_get_info_null_output_and_canary():
 
 
 def test_options_deterministic_values_are_validated_before_any_device():
-    """hspmv_options.deterministic: 0, 1 (ordered), 2 (reproducible); other
-    values, and an explicit column-sorted kernel with 1, are refused while
-    the options are read (HSPMV_E_INVALID), before any device is touched;
-    2 with the column-sorted kernel passes that check."""
+    """hspmv_options.deterministic: 0, 1 (ordered), 2 (reproducible), 3
+    (serial); other values, an explicit column-sorted kernel with 1 or 3 and
+    an explicit vector kernel with 3 are refused (HSPMV_E_INVALID) before any
+    device is touched; 2 with the column-sorted kernel passes that check."""
     import numpy as np
     from hspmv import gen
     L = hspmv.lib()
     A = gen.laplace2d(8, 8)
     cs = A.c_struct()
     h = ctypes.c_void_p()
-    for det, kern, ok in ((3, 0, False), (-1, 0, False), (1, 4, False), (2, 4, True), (1, 0, True)):
+    for det, kern, ok in ((4, 0, False), (-1, 0, False), (1, 4, False), (3, 4, False), (3, 1, False),
+                          (2, 4, True), (1, 0, True), (3, 0, True), (3, 2, True), (3, 3, True)):
         o = _lib.make_options(kern, {"deterministic": det} if det >= 0 else None)
         if det < 0:
             o.deterministic = det
@@ -220,3 +221,4 @@ def test_options_deterministic_values_are_validated_before_any_device():
             L.hspmv_destroy(h)
     assert _lib.make_options(0, {"deterministic": "reproducible"}).deterministic == 2
     assert _lib.make_options(0, {"deterministic": "ordered"}).deterministic == 1
+    assert _lib.make_options(0, {"deterministic": "serial"}).deterministic == 3

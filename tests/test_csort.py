@@ -464,7 +464,7 @@ def test_csort_reproducible_auto_and_option_rules():
     with pytest.raises(hspmv.HspmvError):
         hspmv.SpMV(A, kernel="csort", options={"deterministic": "ordered"})
     with pytest.raises(hspmv.HspmvError):
-        hspmv.SpMV(A, options={"deterministic": 3})
+        hspmv.SpMV(A, options={"deterministic": 4})
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
