@@ -110,8 +110,10 @@ void tuning_from_env(Tuning *) {}
 
 // The kernel rules of hspmv_options.deterministic 1 and 3 (checked at
 // creation, whatever set the mode): no CSORT (its sums do not follow
-// omp_spmv's order); SERIAL also no VECTOR (shuffle trees) and no split rows
-// (their pieces add in a second kernel) -- every row in one lane, in order.
+// omp_spmv's order); SERIAL also no VECTOR (shuffle trees).  SERIAL's rows
+// over kLongRow nonzeros go to hspmv_long_serial (one workgroup per row,
+// still one add at a time in order), or with HSPMV_FLAG_NO_SPLIT stay in the
+// row kernels' lanes.
 int apply_deterministic(unsigned *flags, const Tuning &t) {
   const unsigned k = *flags & 0xFu;
   if ((t.deterministic == HSPMV_DETERMINISTIC_ORDERED || t.deterministic == HSPMV_DETERMINISTIC_SERIAL) &&
@@ -123,7 +125,6 @@ int apply_deterministic(unsigned *flags, const Tuning &t) {
     if (k == kVector)
       return set_error(HSPMV_E_INVALID, "deterministic = 3 (serial order) runs the row kernels only: "
                                         "HSPMV_KERNEL_VECTOR sums each row in a shuffle tree");
-    *flags |= HSPMV_FLAG_NO_SPLIT;
   }
   return HSPMV_OK;
 }

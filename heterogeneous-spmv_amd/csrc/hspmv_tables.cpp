@@ -775,7 +775,16 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
       }
       lcs.push_back((int32_t)(ck.size() / 2));
     }
-    if (!lrow.empty()) {
+    if (!lrow.empty() && s.dp.serial_max == INT32_MAX) {  // serial order: one workgroup per row
+      int rc;
+      const int64_t nl = (int64_t)lrow.size();
+      if ((rc = dev_alloc(&s.d_long_row, 4 * (size_t)nl, &s.bytes))) return rc;
+      HIP_TRY(hipMemcpy(s.d_long_row, lrow.data(), 4 * (size_t)nl, hipMemcpyHostToDevice));
+      s.dp.long_t = kLongRow;
+      s.dp.n_long = (int32_t)nl;
+      s.dp.long_row = s.d_long_row;
+      s.dp.long_serial = true;
+    } else if (!lrow.empty()) {
       int rc;
       const int64_t nl = (int64_t)lrow.size(), nc = (int64_t)ck.size() / 2;
       if ((rc = dev_alloc(&s.d_long_row, 4 * (size_t)nl, &s.bytes))) return rc;

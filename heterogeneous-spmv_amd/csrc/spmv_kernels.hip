@@ -130,6 +130,65 @@ __global__ __launch_bounds__(256) void hspmv_long_reduce(
   if (lane == 0) y[long_row[j]] = s;
 }
 
+// Serial order (hspmv_options.deterministic = 3), rows over kLongRow
+// nonzeros: one 256-thread workgroup per row adds the row's products left
+// to right from 0, as omp_spmv does -- which no number of lanes can share.
+// Waves 1-3 form the next 16 KiB of products (multiply rounded on its
+// own, no fma: -ffp-contract=off) into one LDS buffer while lane 0 of wave 0
+// adds the current one: 32 products per step, read as 16-byte LDS loads
+// issued before the step's dependent adds, so the add chain (not the LDS
+// round trip) bounds the row.  In the row kernels such a row was walked by
+// one lane through its wave's product chunks, one LDS round trip per four
+// adds (C5's 144 616-nonzero hub row: 2.1 ms for the launch).
+constexpr int kLongSerialBytes = 16384;  // per LDS buffer (two: 32 KiB)
+
+template <typename T, bool NT>
+__global__ __launch_bounds__(256) void hspmv_long_serial(
+    int32_t n_long, const int32_t *__restrict__ long_row, const int32_t *__restrict__ rp,
+    const int32_t *__restrict__ ci, const T *__restrict__ val, const T *__restrict__ x,
+    T *__restrict__ y) {
+  constexpr int32_t kLongSerialChunk = kLongSerialBytes / (int)sizeof(T);
+  __shared__ __attribute__((aligned(16))) T buf[2][kLongSerialChunk];
+  const int j = blockIdx.x;
+  if (j >= n_long) return;  // block-uniform
+  const int32_t r = long_row[j];
+  const int32_t k0 = rp[r], k1 = rp[r + 1];
+  auto fill = [&](T *dst, int32_t c, int t, int nt) {
+    const int32_t n = min(k1 - c, kLongSerialChunk);
+    for (int32_t i = t; i < n; i += nt) {
+      const T p = ldg<NT>(val + c + i) * x[ldg<NT>(ci + c + i)];
+      dst[i] = p;
+    }
+  };
+  fill(buf[0], k0, threadIdx.x, 256);
+  __syncthreads();
+  T acc = T(0);
+  int s = 0;
+  for (int32_t c = k0; c < k1; c += kLongSerialChunk, s ^= 1) {
+    if (threadIdx.x >= kWave) {
+      if (c + kLongSerialChunk < k1) fill(buf[s ^ 1], c + kLongSerialChunk, threadIdx.x - kWave, 256 - kWave);
+    } else if (threadIdx.x == 0) {
+      const int32_t n = min(k1 - c, kLongSerialChunk);
+      const T *b = buf[s];
+      constexpr int V = 16 / (int)sizeof(T), B = 32;
+      typedef T tv __attribute__((ext_vector_type(V)));
+      int32_t i = 0;
+      for (; i + B <= n; i += B) {
+        tv q[B / V];
+#pragma unroll
+        for (int v = 0; v < B / V; ++v) q[v] = *reinterpret_cast<const tv *>(b + i + v * V);
+#pragma unroll
+        for (int v = 0; v < B / V; ++v)
+#pragma unroll
+          for (int e = 0; e < V; ++e) acc = acc + q[v][e];
+      }
+      for (; i < n; ++i) acc = acc + b[i];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) y[r] = acc;
+}
+
 // ------------------------------------------------------------------ dispatch
 
 template <typename T, bool NT>
@@ -187,7 +246,11 @@ hipError_t launch_typed(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p,
       return hipErrorInvalidValue;
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (dp.n_long > 0) {
+  if (dp.n_long > 0 && dp.long_serial) {
+    hipLaunchKernelGGL((hspmv_long_serial<T, NT>), dim3((unsigned)dp.n_long), dim3(256), 0, st, dp.n_long,
+                       dp.long_row, rp, ci, val, x, y);
+    e = hipGetLastError();
+  } else if (dp.n_long > 0) {
     hipLaunchKernelGGL((hspmv_long_chunks<T, NT>), dim3((unsigned)dp.n_chunks), dim3(256), 0, st,
                        dp.n_chunks, dp.chunk_k, ci, val, x, static_cast<T *>(dp.partials));
     hipLaunchKernelGGL((hspmv_long_reduce<T>), dim3((unsigned)((dp.n_long + 3) / 4)), dim3(256),

@@ -338,10 +338,12 @@ typedef struct {
                              right from 0, one lane per row, as omp_spmv
                              does (spmv-csr/spmv.c:92-114): y bit-identical
                              to it for every input, at the cost of long rows
-                             summed by one lane (implies HSPMV_FLAG_NO_SPLIT;
-                             VECTOR and CSORT refused; a matrix the row
-                             kernels cannot address fails with
-                             HSPMV_E_INVALID; hspmv_info.serial_order)      */
+                             added one product at a time (rows over 4096
+                             nonzeros: one workgroup each, or with
+                             HSPMV_FLAG_NO_SPLIT their lane; VECTOR and CSORT
+                             refused; a matrix the row kernels cannot
+                             address fails with HSPMV_E_INVALID;
+                             hspmv_info.serial_order)                      */
   int32_t placement_trials; /* array placements timed at creation (0/1
                                off, K <= 8; see hspmv_create_on_device)    */
 } hspmv_options;

@@ -8,9 +8,10 @@ Checked on the GPU, through the C ABI:
   (tests/golden, made by oracle/_ref), long rows included;
 * fp64 against the oracle's omp_spmv restatement (pinned bitwise to the
   reference in tests/test_oracle.py) on matrices with rows of 41 .. 90 000
-  nonzeros (no split rows: the mode implies HSPMV_FLAG_NO_SPLIT), through
-  every row kernel and CSR-3 plan, x slabs, x dictionaries, 32-bit columns
-  and a two-shard handle;
+  nonzeros (those over 4096 added in order by one workgroup each,
+  hspmv_long_serial, or with HSPMV_FLAG_NO_SPLIT by their lane in the row
+  kernels), through every row kernel and CSR-3 plan, x slabs, x
+  dictionaries, 32-bit columns and a two-shard handle;
 * BASELINE configs[4] (C5, 2 M rows, power-law) in fp32 at full size against
   the reference's own omp_spmv (oracle/_ref) when it was built;
 * the mode's refusals and reports (VECTOR / CSORT refused, hspmv_info
@@ -65,7 +66,7 @@ def test_serial_golden_fp32_bitwise_vs_reference_binary_every_row(golden_names):
         x = gen.rand_x(A.n, 42).astype(np.float32)
         for kernel in ("auto", "stream"):
             y, info = run(A, x, kernel=kernel)
-            assert info["serial_order"] == 1 and info["deterministic"] == 1 and info["n_split_rows"] == 0
+            assert info["serial_order"] == 1 and info["deterministic"] == 1
             assert bits_equal(y, g["y_ref_f32_rand"]), (name, kernel)
             if "y_ref_f32_ones" in g:
                 y1, _ = run(A, np.ones(A.n, np.float32), kernel=kernel)
@@ -84,12 +85,19 @@ def test_serial_long_rows_every_kernel_and_plan(dtype):
     cases = [(None, "stream", {}), (None, "auto", {}), (None, "stream", {"x_slabs": 3}),
              (maps, "csr3", {"csr3_plan": "aligned"}), (maps, "csr3", {"csr3_plan": "packed"}),
              (maps, "csr3", {"csr3_plan": "ssr"}), (maps, "csr3", {"x_slabs": 2})]
+    n_long = int((np.diff(A.row_ptr) > 4096).sum())
     for mp, kernel, opts in cases:
         y, info = run(A, x, mp, opts, kernel=kernel)
-        assert info["serial_order"] == 1 and info["n_split_rows"] == 0, (kernel, opts)
+        # rows over 4096 nonzeros: one workgroup each (hspmv_long_serial)
+        assert info["serial_order"] == 1 and info["n_split_rows"] == n_long, (kernel, opts)
         assert bits_equal(y, ref), (kernel, opts, int(np.flatnonzero(y != ref)[0]))
     y, _ = run(A, x, col16=False)
     assert bits_equal(y, ref)
+    # HSPMV_FLAG_NO_SPLIT: the long rows stay in the row kernels' lanes
+    for mp, kernel in ((None, "stream"), (maps, "csr3")):
+        y, info = run(A, x, mp, kernel=kernel, split_rows=False)
+        assert info["serial_order"] == 1 and info["n_split_rows"] == 0
+        assert bits_equal(y, ref), kernel
 
 
 def test_serial_dictionaries_stencil_and_mid_density():
