@@ -7,7 +7,9 @@ clustered columns, sorted or unsorted columns with duplicates, exact zeros,
 m and n from 1 up, fp32 or fp64.  Every case runs AUTO, STREAM, VECTOR (a
 random lane count), CSR3 with freshly built maps under the aligned / packed /
 ssr plans, csort (auto, 4 column parts, and reproducible fixed-point sums:
-bit-identical on a second launch), AUTO with deterministic = 1,
+bit-identical on a second launch), AUTO with deterministic = 1, the serial
+order (deterministic = 3: AUTO, CSR3 under a random plan, STREAM with split
+rows kept whole -- bitwise equal to omp_spmv on EVERY row),
 STREAM with split rows kept whole, AUTO over 2 x slabs, and AUTO over three
 row-range shards, each twice (two x vectors through one handle: no state may
 leak from one launch into the next).
@@ -90,11 +92,17 @@ def runs(A, rng):
         yield "csr3-aligned", {"maps": maps, "kernel": "csr3"}
         yield "csr3-packed", {"maps": maps, "kernel": "csr3", "options": {"csr3_plan": "packed"}}
         yield "csr3-ssr", {"maps": maps, "kernel": "csr3", "options": {"csr3_plan": "ssr"}}
+        yield "csr3-serial", {"maps": maps, "kernel": "csr3",
+                              "options": {"csr3_plan": str(rng.choice(["aligned", "packed", "ssr"])),
+                                          "deterministic": "serial"}}
     yield "csort", {"kernel": "csort"}
     yield "csort-4parts", {"kernel": "csort", "options": {"csort_parts": 4}}
     yield "csort-repro", {"kernel": "csort", "options": {"deterministic": "reproducible"}}
     yield "auto-det", {"options": {"deterministic": 1}}
     yield "stream-whole-rows", {"kernel": "stream", "split_rows": False}
+    yield "auto-serial", {"options": {"deterministic": "serial"}}
+    yield "stream-serial-whole-rows", {"kernel": "stream", "split_rows": False,
+                                       "options": {"deterministic": "serial"}}
     yield "auto-2slabs", {"options": {"x_slabs": 2}}
     yield "sharded-3", {"devices": [0, 0, 0]}  # row-range shards (one device, repeated)
 
@@ -111,7 +119,7 @@ def fixed_point_term(A, x):
     return lens * 2.0 ** -48 * vmax * xmax
 
 
-def check(A, x, y, ordered, what, fixed=False):
+def check(A, x, y, ordered, what, fixed=False, serial=False):
     y64 = oracle.spmv(A.row_ptr, A.col_idx, A.val.astype(np.float64), x.astype(np.float64))
     absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
     lens = np.diff(A.row_ptr)
@@ -122,9 +130,9 @@ def check(A, x, y, ordered, what, fixed=False):
         assert np.all(err <= tol), (what, float(err.max()))
     else:
         assert np.all(err <= (lens + 2) * 2.0 ** -23 * absrow + fx + 1e-30), (what, float(err.max()))
-    if ordered:  # omp_spmv's bits on the short rows
+    if ordered:  # omp_spmv's bits on the short rows (serial order: on every row)
         yo = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
-        short = lens <= SERIAL_MAX
+        short = lens <= (np.iinfo(np.int64).max if serial else SERIAL_MAX)
         u = np.uint64 if y.dtype == np.float64 else np.uint32
         bad = np.flatnonzero(y[short].view(u) != yo[short].view(u))
         assert bad.size == 0, (what, int(np.flatnonzero(short)[bad[0]]))
@@ -144,13 +152,17 @@ def test_fuzz_every_kernel_matches_oracle(seed):
         with op:
             name = op.info["kernel_name"]
             fixed = op.info["csort_fixed_point"] == 1
+            serial = op.info["serial_order"] == 1
+            assert serial == ("serial" in label), (desc, label)
             for i, x in enumerate(xs):
                 y = op(x)
-                check(A, x, y, name in ("stream", "csr3"), (desc, label, name, i), fixed)
+                check(A, x, y, name in ("stream", "csr3"), (desc, label, name, i), fixed, serial)
                 if fixed:  # reproducible: the same bits again
                     assert np.array_equal(op(x).view(np.uint8), y.view(np.uint8)), (desc, label, i)
         if label == "csort-repro" and name == "csort":
             name = "csort-fixed" if fixed else name
+        if serial:
+            name = name + "-serial"
         ran.append((label, name))
         SEEN.add(name)
     assert len(ran) >= 10, (desc, ran)
@@ -160,4 +172,4 @@ def test_fuzz_ran_every_kernel():
     """The forced kernels really ran somewhere in the cases above."""
     if len(SEEN) == 0:
         pytest.skip("run with the fuzz cases")
-    assert {"stream", "vector", "csr3", "csort", "csort-fixed"} <= SEEN, SEEN
+    assert {"stream", "vector", "csr3", "csort", "csort-fixed", "stream-serial", "csr3-serial"} <= SEEN, SEEN
