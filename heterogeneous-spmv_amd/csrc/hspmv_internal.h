@@ -170,6 +170,10 @@ struct DevPlan {
   int32_t serial_max = kSerialMax;  // rows up to this length are summed serially
   int32_t n_long = 0, n_chunks = 0;
   bool long_serial = false;  // split rows summed in order by hspmv_long_serial (deterministic = 3)
+  // ... on a stream of their own, forked from and joined back into the
+  // launch stream, so they run beside the row kernel instead of after it
+  hipStream_t long_stream = nullptr;
+  hipEvent_t long_fork = nullptr, long_join = nullptr;
   const int32_t *long_row = nullptr;    // n_long row ids (shard-local)
   const int32_t *long_cstart = nullptr; // n_long+1, chunk ranges per split row
   const int32_t *chunk_k = nullptr;     // 2*n_chunks: [k0, k1) per chunk

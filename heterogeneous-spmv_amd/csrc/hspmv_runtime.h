@@ -87,6 +87,8 @@ struct Shard {
   const void *x = nullptr; // x in use (own or bound)
   void *y = nullptr;       // y in use (own or bound)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipStream_t long_stream = nullptr;  // serial order: the long-row kernel's stream
+  hipEvent_t long_fork = nullptr, long_join = nullptr;
   int64_t bytes = 0;
   int64_t x_entries = 0;   // distinct columns of this shard
   double c16_saved = 0.0;  // bytes per SpMV the 16-bit column offsets save

@@ -70,6 +70,9 @@ void free_shard(Shard &s, bool borrowed) {
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
   if (s.own_stream && s.stream) (void)hipStreamDestroy(s.stream);
+  if (s.long_fork) (void)hipEventDestroy(s.long_fork);
+  if (s.long_join) (void)hipEventDestroy(s.long_join);
+  if (s.long_stream) (void)hipStreamDestroy(s.long_stream);
   s = Shard();
 }
 

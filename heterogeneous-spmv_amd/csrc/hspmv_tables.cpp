@@ -779,11 +779,19 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
       int rc;
       const int64_t nl = (int64_t)lrow.size();
       if ((rc = dev_alloc(&s.d_long_row, 4 * (size_t)nl, &s.bytes))) return rc;
+      if ((rc = dev_alloc(&s.d_partials, dtype_size(dtype) * (size_t)nl, &s.bytes))) return rc;
       HIP_TRY(hipMemcpy(s.d_long_row, lrow.data(), 4 * (size_t)nl, hipMemcpyHostToDevice));
+      s.dp.partials = s.d_partials;  // the rows' sums, scattered into y after the row kernel
       s.dp.long_t = kLongRow;
       s.dp.n_long = (int32_t)nl;
       s.dp.long_row = s.d_long_row;
       s.dp.long_serial = true;
+      HIP_TRY(hipStreamCreateWithFlags(&s.long_stream, hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&s.long_fork, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&s.long_join, hipEventDisableTiming));
+      s.dp.long_stream = s.long_stream;
+      s.dp.long_fork = s.long_fork;
+      s.dp.long_join = s.long_join;
     } else if (!lrow.empty()) {
       int rc;
       const int64_t nl = (int64_t)lrow.size(), nc = (int64_t)ck.size() / 2;

@@ -136,8 +136,8 @@ __global__ __launch_bounds__(256) void hspmv_long_reduce(
 // Waves 1-3 form the next 16 KiB of products (multiply rounded on its
 // own, no fma: -ffp-contract=off) into one LDS buffer while lane 0 of wave 0
 // adds the current one: 32 products per step, read as 16-byte LDS loads
-// issued before the step's dependent adds, so the add chain (not the LDS
-// round trip) bounds the row.  In the row kernels such a row was walked by
+// issued one step ahead of the dependent adds, so the add chain (not the
+// LDS round trip) bounds the row.  In the row kernels such a row was walked by
 // one lane through its wave's product chunks, one LDS round trip per four
 // adds (C5's 144 616-nonzero hub row: 2.1 ms for the launch).
 constexpr int kLongSerialBytes = 16384;  // per LDS buffer (two: 32 KiB)
@@ -146,7 +146,7 @@ template <typename T, bool NT>
 __global__ __launch_bounds__(256) void hspmv_long_serial(
     int32_t n_long, const int32_t *__restrict__ long_row, const int32_t *__restrict__ rp,
     const int32_t *__restrict__ ci, const T *__restrict__ val, const T *__restrict__ x,
-    T *__restrict__ y) {
+    T *__restrict__ y, T *__restrict__ lsum) {
   constexpr int32_t kLongSerialChunk = kLongSerialBytes / (int)sizeof(T);
   __shared__ __attribute__((aligned(16))) T buf[2][kLongSerialChunk];
   const int j = blockIdx.x;
@@ -173,20 +173,51 @@ __global__ __launch_bounds__(256) void hspmv_long_serial(
       constexpr int V = 16 / (int)sizeof(T), B = 32;
       typedef T tv __attribute__((ext_vector_type(V)));
       int32_t i = 0;
-      for (; i + B <= n; i += B) {
-        tv q[B / V];
+      // two register sets, no copies: each step's loads go out (a
+      // sched_barrier keeps them there) before the other set's adds
+      auto load = [&](tv(&q)[B / V], int32_t at) {
 #pragma unroll
-        for (int v = 0; v < B / V; ++v) q[v] = *reinterpret_cast<const tv *>(b + i + v * V);
+        for (int v = 0; v < B / V; ++v) q[v] = *reinterpret_cast<const tv *>(b + at + v * V);
+      };
+      auto add = [&](const tv(&q)[B / V]) {
 #pragma unroll
         for (int v = 0; v < B / V; ++v)
 #pragma unroll
           for (int e = 0; e < V; ++e) acc = acc + q[v][e];
+      };
+      if (n >= 2 * B) {
+        tv q0[B / V], q1[B / V];
+        load(q0, 0);
+        for (; i + 2 * B <= n; i += 2 * B) {
+          load(q1, i + B);
+          __builtin_amdgcn_sched_barrier(0);
+          add(q0);
+          __builtin_amdgcn_sched_barrier(0);
+          load(q0, i + 3 * B <= n ? i + 2 * B : i);  // (a harmless reload at the end)
+          __builtin_amdgcn_sched_barrier(0);
+          add(q1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       for (; i < n; ++i) acc = acc + b[i];
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) y[r] = acc;
+  if (threadIdx.x == 0) {
+    if (lsum)
+      lsum[j] = acc;  // forked: hspmv_long_scatter writes y after the row kernel
+    else
+      y[r] = acc;
+  }
+}
+
+// The forked long rows' sums into y, on the launch stream after the row
+// kernel (whose x-slab passes also write those rows: empty segments).
+template <typename T>
+__global__ __launch_bounds__(256) void hspmv_long_scatter(int32_t n_long, const int32_t *__restrict__ long_row,
+                                                          const T *__restrict__ lsum, T *__restrict__ y) {
+  const int32_t j = (int32_t)(blockIdx.x * 256 + threadIdx.x);
+  if (j < n_long) y[long_row[j]] = lsum[j];
 }
 
 // ------------------------------------------------------------------ dispatch
@@ -199,6 +230,20 @@ hipError_t launch_typed(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p,
   const int32_t *ci = A.col_idx;
   const T *val = static_cast<const T *>(A.val);
   hipError_t e = hipSuccess;
+  // serial order: the long rows' workgroups start first, on their own
+  // stream (forked from st, joined back below), beside the row kernel, and
+  // leave their sums in dp.partials for hspmv_long_scatter -- C5: 289 us of
+  // x-slab passes and a 497 us add chain otherwise in sequence
+  const bool fork = dp.n_long > 0 && dp.long_serial && dp.long_stream;
+  if (fork) {
+    if ((e = hipEventRecord(dp.long_fork, st)) != hipSuccess ||
+        (e = hipStreamWaitEvent(dp.long_stream, dp.long_fork, 0)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL((hspmv_long_serial<T, NT>), dim3((unsigned)dp.n_long), dim3(256), 0, dp.long_stream,
+                       dp.n_long, dp.long_row, rp, ci, val, x, y, static_cast<T *>(dp.partials));
+    if ((e = hipGetLastError()) != hipSuccess || (e = hipEventRecord(dp.long_join, dp.long_stream)) != hipSuccess)
+      return e;
+  }
   switch (p.kernel) {
     case kVector:
       switch (p.lanes) {
@@ -246,9 +291,14 @@ hipError_t launch_typed(const DevCSR &A, const DevPlan &dp, const LaunchPlan &p,
       return hipErrorInvalidValue;
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (dp.n_long > 0 && dp.long_serial) {
+  if (fork) {
+    if ((e = hipStreamWaitEvent(st, dp.long_join, 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL((hspmv_long_scatter<T>), dim3((unsigned)((dp.n_long + 255) / 256)), dim3(256), 0, st,
+                       dp.n_long, dp.long_row, static_cast<const T *>(dp.partials), y);
+    e = hipGetLastError();
+  } else if (dp.n_long > 0 && dp.long_serial) {
     hipLaunchKernelGGL((hspmv_long_serial<T, NT>), dim3((unsigned)dp.n_long), dim3(256), 0, st, dp.n_long,
-                       dp.long_row, rp, ci, val, x, y);
+                       dp.long_row, rp, ci, val, x, y, static_cast<T *>(nullptr));
     e = hipGetLastError();
   } else if (dp.n_long > 0) {
     hipLaunchKernelGGL((hspmv_long_chunks<T, NT>), dim3((unsigned)dp.n_chunks), dim3(256), 0, st,
