@@ -46,6 +46,12 @@ for f in $G/*.csr $D/powerlaw.csr $D/banded.csr $D/stencil.csr; do
   step "csr_${b}_det" $B/spmv-csr $f 3 --deterministic --x rand:1
   step "csr_${b}_repro" $B/spmv-csr $f 3 --kernel csort --reproducible --x rand:1
   step "csr_${b}_repro_f32" $B/spmv-csr $f 3 --kernel csort --reproducible --dtype f32 --x rand:1
+  step "csr_${b}_serial" $B/spmv-csr $f 3 --serial --x rand:1
+  step "csr_${b}_serial_f32" $B/spmv-csr $f 3 --serial --dtype f32 --x rand:1
+done
+for f in $G/*.csr3; do
+  b=$(basename $f .csr3)
+  step "csrk_${b}_serial" $B/spmv-csrk $f 3 --serial --plan ssr --x rand:2
 done
 for f in $G/*.csr3; do
   b=$(basename $f .csr3)
