@@ -24,7 +24,7 @@ int check_handle(hspmv_handle *h) {
 int create_single(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps *maps, int device,
                   void *stream, unsigned flags, const Tuning &tune) {
   ContigScope contig(tune);
-  if (int rc0 = apply_deterministic(&flags, tune)) return rc0;
+  if (int rc0 = check_deterministic(flags, tune)) return rc0;
   const bool devptrs = (flags & HSPMV_FLAG_DEVICE_PTRS) != 0;
   if (!A) return set_error(HSPMV_E_INVALID, "matrix is NULL");
   int ndev = 0;

@@ -25,7 +25,7 @@ int create_sharded(hspmv_handle **hp, const hspmv_csr *A, const hspmv_csr3_maps 
   ContigScope contig(tune);
   const int num_gpus = (int)devs.size();
   int rc;
-  if ((rc = apply_deterministic(&flags, tune))) return rc;
+  if ((rc = check_deterministic(flags, tune))) return rc;
   if ((rc = validate_host_csr(A, true))) return rc;
   if ((rc = validate_host_maps(maps, A->m))) return rc;
   const bool csr3 = maps && maps->n_ssr > 0;

@@ -114,8 +114,8 @@ void tuning_from_env(Tuning *) {}
 // over kLongRow nonzeros go to hspmv_long_serial (one workgroup per row,
 // still one add at a time in order), or with HSPMV_FLAG_NO_SPLIT stay in the
 // row kernels' lanes.
-int apply_deterministic(unsigned *flags, const Tuning &t) {
-  const unsigned k = *flags & 0xFu;
+int check_deterministic(unsigned flags, const Tuning &t) {
+  const unsigned k = flags & 0xFu;
   if ((t.deterministic == HSPMV_DETERMINISTIC_ORDERED || t.deterministic == HSPMV_DETERMINISTIC_SERIAL) &&
       k == kCsort)
     return set_error(HSPMV_E_INVALID, "the column-sorted kernel (HSPMV_KERNEL_CSORT) does not sum in "

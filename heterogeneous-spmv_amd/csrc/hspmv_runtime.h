@@ -137,7 +137,7 @@ constexpr double kMallResident = 192.0 * 1024 * 1024;
 int tuning_from_options(const hspmv_options *o, Tuning *t);
 void tuning_from_env(Tuning *t);
 Tuning default_tuning();
-int apply_deterministic(unsigned *flags, const Tuning &t);
+int check_deterministic(unsigned flags, const Tuning &t);
 
 // ---- hspmv_shard.cpp
 extern thread_local bool t_contig;
