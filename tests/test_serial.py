@@ -150,20 +150,26 @@ def test_serial_refusals():
             hspmv.SpMV(A, kernel=kernel, options=SERIAL)
 
 
-def test_config_c5_serial_fp32_bitwise_vs_reference_omp_spmv():
-    """BASELINE configs[4] at full size in fp32: y bit-identical to the
-    reference's own omp_spmv (oracle/_ref, spmv-csr/spmv.c built unmodified)
-    on all 2 M rows, long hub rows included."""
-    A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32)
+@pytest.mark.parametrize("rcm", [False, True])
+def test_config_c5_serial_fp32_bitwise_vs_reference_omp_spmv(rcm):
+    """BASELINE configs[4] at full size in fp32, and its RCM ordering (the
+    reference's input convention): y bit-identical to the reference's own
+    omp_spmv (oracle/_ref, spmv-csr/spmv.c built unmodified) on all 2 M
+    rows, long hub rows included; and again on a second SpMV (the forked
+    long-row stream leaves no state behind)."""
+    A = gen.powerlaw(2_000_000, seed=1234, dtype=np.float32, rcm=rcm)
     maps = hspmv.build_csr3_maps(A, *hspmv.csr3_params(A.nnz / A.m, "mi355x"))
     x = gen.rand_x(A.n, 21).astype(np.float32)
     y_ref = oracle.ref_spmv(A.row_ptr, A.col_idx, A.val, x) if oracle.ref_available() else \
         oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
-    y, info = run(A, x, maps)
-    assert info["kernel_name"] in ("stream", "csr3") and info["serial_order"] == 1
     assert np.diff(A.row_ptr).max() > 4096  # the hub rows a default handle splits
-    bad = np.flatnonzero(y.view(np.uint32) != y_ref.view(np.uint32))
-    assert bad.size == 0, (bad.size, int(bad[0]))
+    with hspmv.SpMV(A, maps, options=SERIAL) as op:
+        info = op.info
+        assert info["kernel_name"] in ("stream", "csr3") and info["serial_order"] == 1
+        for _ in range(2):
+            y = op(x)
+            bad = np.flatnonzero(y.view(np.uint32) != y_ref.view(np.uint32))
+            assert bad.size == 0, (bad.size, int(bad[0]))
 
 
 def test_cli_serial_reports_bitwise():
