@@ -222,3 +222,14 @@ def test_options_deterministic_values_are_validated_before_any_device():
     assert _lib.make_options(0, {"deterministic": "reproducible"}).deterministic == 2
     assert _lib.make_options(0, {"deterministic": "ordered"}).deterministic == 1
     assert _lib.make_options(0, {"deterministic": "serial"}).deterministic == 3
+
+
+def test_deterministic_names_match_the_header():
+    """hspmv._lib.DETERMINISTIC (the names the Python layer and tests use)
+    carries the header's HSPMV_DETERMINISTIC_* values."""
+    import re as _re
+    text = _lib.HEADER.read_text()
+    vals = {k.lower(): int(v) for k, v in _re.findall(r"#define HSPMV_DETERMINISTIC_(\w+) (\d+)", text)}
+    assert vals == {"ordered": 1, "reproducible": 2, "serial": 3}
+    for name, v in vals.items():
+        assert _lib.DETERMINISTIC[name] == v
