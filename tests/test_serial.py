@@ -73,6 +73,23 @@ def test_serial_golden_fp32_bitwise_vs_reference_binary_every_row(golden_names):
                 assert bits_equal(y1, g["y_ref_f32_ones"]), (name, kernel)
 
 
+def test_serial_golden_csr3_fixtures_every_plan(manifest):
+    """The golden .csr3 files (their maps as written) under each CSR3 plan,
+    fp64 and fp32: the CSR-3 CPU loop's bits (oracle csr3_spmv, csrk.cpp:
+    247-285, equal to omp_spmv row by row) on every row."""
+    for name, ent in manifest["fixtures"].items():
+        if "csr3" not in ent:
+            continue
+        for dt in (np.float64, np.float32):
+            A, maps = hspmv.read_csr3(GOLDEN / f"{name}.csr3", dt)
+            x = gen.rand_x(A.n, 42).astype(dt)
+            ref = oracle.csr3_spmv(maps.outer, maps.inner, A.row_ptr, A.col_idx, A.val, x)
+            for plan in ("aligned", "packed", "ssr"):
+                y, info = run(A, x, maps, {"csr3_plan": plan}, kernel="csr3")
+                assert info["kernel_name"] == "csr3" and info["serial_order"] == 1
+                assert bits_equal(y, ref), (name, dt, plan)
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_serial_long_rows_every_kernel_and_plan(dtype):
     """Rows of 41 .. 90 000 nonzeros (default handles split those over 4096
