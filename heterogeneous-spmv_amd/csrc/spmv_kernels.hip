@@ -21,6 +21,11 @@
 //          (shuffle tree), accumulated over chunks (fp64 tolerance);
 //        - split rows (> kLongRow nonzeros) are skipped here and summed by
 //          hspmv_long_chunks + hspmv_long_reduce (many workgroups per row).
+//      The serial bound is an argument (DevPlan.serial_max): with
+//      hspmv_options.deterministic = 3 every row takes the first branch,
+//      and split rows go to hspmv_long_serial (one workgroup per row, the
+//      adds still in order, on a stream forked beside this kernel) +
+//      hspmv_long_scatter.
 //      Replaces cuda_spmv's thread-per-row scalar loop (uncoalesced) with a
 //      CSR-stream scheme (coalesced stream + LDS segmented sums).
 //
