@@ -148,3 +148,26 @@ def test_fixedpoint_model_fp64_is_within_its_bound():
     bound = lens * 2.0 ** -49 * vmax * np.abs(x).max() + (lens + 3) * 2.0 ** -53 * absrow + 1e-300
     ok = lens <= 4096
     assert np.all(np.abs(y[ok] - y64[ok]) <= bound[ok])
+
+
+def test_fixedpoint_model_exact_q_is_half_even_of_the_exact_product():
+    """fixedpoint_model.exact_q (the fp64 branch's product rounding) against
+    Python's exact rationals: rint(v x 2^E), ties to even, on values spread
+    over 60 binades, zeros, signs, and exact ties."""
+    from fractions import Fraction
+
+    import numpy as np
+    from fixedpoint_model import FIX_BITS, exact_q, xexp_of
+    rng = np.random.default_rng(1)
+    v = rng.uniform(-1, 1, 3000) * np.exp2(-rng.integers(0, 60, 3000))
+    x = rng.standard_normal(3000) * 3
+    v[::7] = 0.0
+    E = FIX_BITS - xexp_of(x)
+    # exact ties: (5/8 or 7/8) * 4 * 2^-E -> 2.5 / 3.5 units (to 2 and 4)
+    v[1::22], v[12::22] = 0.625, -0.875
+    x[1::11] = np.ldexp(4.0, -E)
+    assert xexp_of(x) == FIX_BITS - E
+    q = exact_q(v, x, E)
+    assert set(q[1::22].tolist()) == {2} and set(q[12::22].tolist()) == {-4}
+    for a, b, qq in zip(v, x, q):
+        assert int(qq) == round(Fraction(float(a)) * Fraction(float(b)) * 2 ** E), (a, b)
