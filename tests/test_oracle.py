@@ -171,3 +171,37 @@ def test_fixedpoint_model_exact_q_is_half_even_of_the_exact_product():
     assert set(q[1::22].tolist()) == {2} and set(q[12::22].tolist()) == {-4}
     for a, b, qq in zip(v, x, q):
         assert int(qq) == round(Fraction(float(a)) * Fraction(float(b)) * 2 ** E), (a, b)
+
+
+def test_fixedpoint_model_parts_small_exact():
+    """reproducible_csort_y on a tiny matrix against a direct restatement in
+    rationals: per column part, the integer sum of the rounded scaled
+    products, converted and scaled, rounded to fp32; the parts added in
+    order in fp64 and rounded (the kernel's finishing pass)."""
+    from fractions import Fraction
+
+    import numpy as np
+    from fixedpoint_model import FIX_BITS, reproducible_csort_y, row_scales, xexp_of
+    rng = np.random.default_rng(4)
+    m, n = 40, 30
+    lens = rng.integers(0, 12, m)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ci = np.concatenate([np.sort(rng.choice(n, ln, replace=False)) for ln in lens]).astype(np.int64)
+    val = (rng.standard_normal(rp[-1]) * np.exp2(rng.integers(-8, 8, rp[-1]))).astype(np.float32)
+    x = rng.standard_normal(n).astype(np.float32)
+    pb = (0, 11, 23)
+    y = reproducible_csort_y(rp, ci, val, x, pb)
+    E = FIX_BITS - xexp_of(x)
+    rexp = row_scales(rp, val)
+    for r in range(m):
+        acc = 0.0
+        for h in range(len(pb)):
+            lo, hi = pb[h], (pb[h + 1] if h + 1 < len(pb) else n)
+            s = 0
+            for k in range(rp[r], rp[r + 1]):
+                if lo <= ci[k] < hi:
+                    vs = Fraction(float(np.float32(np.ldexp(val[k], int(rexp[r])))))
+                    s += round(vs * Fraction(float(x[ci[k]])) * 2 ** E)
+            p = np.float32(np.ldexp(float(s), int(-E - rexp[r])))
+            acc = acc + float(p)
+        assert np.float32(acc).tobytes() == y[r].tobytes(), r
