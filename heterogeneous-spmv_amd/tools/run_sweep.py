@@ -19,7 +19,8 @@ tuning mode (--sizes) adds the reference's "(ssrs srs)" column for spmv-csrk
 manual sizes, as run_tuning.py:126 does.
 
     python heterogeneous-spmv_amd/tools/run_sweep.py --matrices DIR [--drivers spmv-csr,spmv-csrk]
-        [--schedules auto,stream,csr3,vector] [--gpus 1] [--num-runs 20]
+        [--schedules auto,stream,csr3,vector,csort,ordered,reproducible,serial]
+        [--gpus 1] [--num-runs 20]
         [--sizes 20x10,7x8] [--out DIR] [--record sweep.csv] [--timeout 600]
     python .../run_sweep.py --synthetic c2,c3 ...   # writes the configs as .csr first
     python .../run_sweep.py --mtx DIR [--csr3] ...   # SuiteSparse .mtx files first
@@ -46,6 +47,9 @@ BUILD = HERE.parent / "build"
 SCHEDULES = {  # schedule name -> driver options
     "auto": [], "stream": ["--kernel", "stream"], "csr3": ["--kernel", "csr3"],
     "vector": ["--kernel", "vector"], "nt": ["--kernel", "stream", "--nt"],
+    "csort": ["--kernel", "csort"],
+    # the summation contracts (hspmv_options.deterministic 1 / 2 / 3)
+    "ordered": ["--deterministic"], "reproducible": ["--reproducible"], "serial": ["--serial"],
 }
 
 
