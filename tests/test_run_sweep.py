@@ -96,6 +96,15 @@ def test_sweep_on_golden_matrices(tmp_path):
         t = [float(v) for v in (r[5:8] if r[0] == "spmv-csrk" else r[4:7])]
         assert 0 < t[0] <= t[2] <= t[1]
         assert r[-2] == "PASS"
+    # the summation contracts as schedules; the serial one also bitwise
+    out2 = tmp_path / "out2"
+    rc = run_sweep.main(["--matrices", str(d), "--out", str(out2), "--num-runs", "3", "--drivers", "spmv-csr",
+                         "--schedules", "ordered,reproducible,serial"])
+    assert rc == 0
+    rows = [r.split(", ") for r in (out2 / "sweep.csv").read_text().splitlines()]
+    assert len(rows) == 2 * 3 and all(r[-2] == "PASS" for r in rows), rows
+    logs = list((out2 / "runs" / "spmv-csr").glob("*_serial_*.txt"))
+    assert logs and all("Bitwise: 0 rows differ" in f.read_text() for f in logs)
 
 
 def test_mtx_inputs_are_converted_first(tmp_path):
