@@ -58,6 +58,7 @@ struct Tuning {
   int csort_u = 0;          // 0 auto, 4/8/16
   int stream_waves = 0;     // 0 auto, 1/2/4
   int deterministic = 0;    // 1: ordered row kernels (omp_spmv's order); 2: reproducible (fixed-point csort allowed)
+  int serial_max = 0;       // A/B: the row kernels' serial bound (0: kSerialMax)
   int placement_trials = 0; // 0/1 off, K <= 8 array sets
   int ssr_w = 0;            // SSR plan waves per workgroup (0: ssr_waves(); A/B)
   int ssr_align = -1;       // SSR plan wave cut: 2 row-granular nnz balance (-1: default), 0 super-rows, 1 aligned pieces

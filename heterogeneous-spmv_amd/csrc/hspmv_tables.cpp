@@ -752,6 +752,8 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
       return set_error(HSPMV_E_INVALID, "deterministic = 3 (serial order) needs the row kernels, and "
                                         "they cannot address this matrix (32-bit offsets)");
     s.dp.serial_max = INT32_MAX;
+  } else if (s.tune.serial_max > 0) {
+    s.dp.serial_max = s.tune.serial_max;  // A/B knob (HSPMV_SERIAL_MAX, diagnostic builds)
   }
   int64_t long_nnz = 0;
   if (s.plan.kernel == kCsort) {  // long rows are slices of the csort blocks
