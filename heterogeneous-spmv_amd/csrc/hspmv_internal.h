@@ -100,6 +100,11 @@ constexpr int32_t kLongRow = 4096;
 // one lane in the row kernels; longer ones cooperatively (fixed DPP trees) --
 // unless DevPlan.serial_max raises the bound (deterministic = 3).
 constexpr int32_t kSerialMax = 40;
+// fp32 data: 48 -- rows of 41-48 nonzeros summed serially ran 15-27 % faster
+// than in the cooperative trees (d41 113.7 -> 83.0 us, d48 106.3 -> 90.2),
+// with every other shape flat (profiles/r06s3/ab_serial48_f32.jsonl); fp64
+// rows of 48 serially met in LDS banks (d48 +41 %, r06s2), so fp64 keeps 40.
+constexpr int32_t kSerialMaxF32 = 48;
 constexpr int32_t kLongChunk = 4096;
 
 // Column-sorted row blocks (csort.hip): workgroup b works on column part
@@ -168,7 +173,7 @@ struct DevPlan {
   int32_t task_align = 0;
   // split rows
   int32_t long_t = 0x7fffffff;  // rows with more nonzeros are split rows
-  int32_t serial_max = kSerialMax;  // rows up to this length are summed serially
+  int32_t serial_max = kSerialMax;  // rows up to this length are summed serially (fp32: kSerialMaxF32)
   int32_t n_long = 0, n_chunks = 0;
   bool long_serial = false;  // split rows summed in order by hspmv_long_serial (deterministic = 3)
   // ... on a stream of their own, forked from and joined back into the

@@ -747,6 +747,7 @@ int build_plan_tables(Shard &s, int dtype, unsigned flags) {
   const std::vector<int32_t> &rp = s.h_rp;
   const int64_t m = s.A.m;
   s.dp = DevPlan();
+  s.dp.serial_max = dtype == HSPMV_F32 ? kSerialMaxF32 : kSerialMax;
   if (s.tune.deterministic == HSPMV_DETERMINISTIC_SERIAL) {  // every row by one lane, in order
     if (s.plan.kernel != kStream && s.plan.kernel != kCsr3)
       return set_error(HSPMV_E_INVALID, "deterministic = 3 (serial order) needs the row kernels, and "

@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 KERNELS = [("stream", 0), ("vector", 1), ("vector", 2), ("vector", 4), ("vector", 8),
            ("vector", 16), ("vector", 32), ("vector", 64), ("auto", 0)]
 SERIAL_MAX = 40  # rows up to this length go through the ordered (bit-exact) path
+SERIAL_MAX_F32 = 48  # fp32 data: up to 48 (hspmv_internal.h kSerialMaxF32)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -49,11 +50,11 @@ def short_rows(A):
 
 def test_golden_fp32_bitwise_vs_reference_binary(golden_names):
     """STREAM / CSR3 in fp32 reproduce the reference's own omp_spmv output
-    bit for bit on every row of up to 40 nonzeros (x = 1 and x = rand)."""
+    bit for bit on every row of up to 48 nonzeros (x = 1 and x = rand)."""
     for name in golden_names:
         A = hspmv.read_csr(GOLDEN / f"{name}.csr", np.float32)
         g = load_golden(name)
-        ok = short_rows(A)
+        ok = np.diff(A.row_ptr) <= SERIAL_MAX_F32
         x = gen.rand_x(A.n, 42).astype(np.float32)
         for kernel in ("stream", "auto"):
             y, _ = gpu_spmv(A, x, kernel=kernel)
@@ -67,6 +68,30 @@ def test_golden_fp32_bitwise_vs_reference_binary(golden_names):
                 nrow = np.diff(A.row_ptr)
                 err = np.abs(y.astype(np.float64) - g["y_ref_f32_rand"])
                 assert np.all(err <= (nrow + 2) * 2.0 ** -23 * absrow + 1e-30)
+
+
+@pytest.mark.parametrize("k", [41, 44, 48, 49])
+def test_fp32_rows_of_41_to_48_serial(k):
+    """fp32 rows of up to kSerialMaxF32 = 48 nonzeros are summed serially
+    (omp_spmv's bits), 49 cooperatively (within the reference's own error):
+    mid-density banded rows through AUTO / STREAM / CSR3, against the
+    oracle's omp_spmv restatement (pinned bitwise to the reference)."""
+    rng = np.random.default_rng(k)
+    m, n = 60_000, 60_000
+    lens = np.full(m, k)
+    rp = np.concatenate([[0], np.cumsum(lens)])
+    ci = (np.arange(m)[:, None] + np.arange(k)[None, :] * 3) % n
+    ci.sort(axis=1)
+    A = hspmv.CsrMatrix(m, n, rp, ci.reshape(-1).astype(np.int32), rng.uniform(-1, 1, m * k).astype(np.float32))
+    x = gen.rand_x(n, 5).astype(np.float32)
+    ref = oracle.spmv(A.row_ptr, A.col_idx, A.val, x)
+    for kernel in ("auto", "stream", "csr3"):
+        y, _ = gpu_spmv(A, x, kernel=kernel)
+        if k <= SERIAL_MAX_F32:
+            assert np.array_equal(y.view(np.uint32), ref.view(np.uint32)), (k, kernel)
+        else:
+            absrow = oracle.abs_rowsum(A.row_ptr, A.col_idx, A.val, x)
+            assert np.all(np.abs(y.astype(np.float64) - ref) <= (k + 2) * 2.0 ** -23 * absrow + 1e-30)
 
 
 def test_golden_fp64_all_kernels(golden_names):
