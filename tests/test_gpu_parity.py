@@ -4,7 +4,7 @@ Bar (BASELINE.json north star): fp64 y within
     |y - y64| <= 1e-6 |y64| + 1e-12 * sum_k |a_k x_k|
 of the spmv-csr restatement.  The STREAM / CSR3 kernels sum each row in the
 reference order with the reference rounding, so on rows up to 40 nonzeros
-(SERIAL_MAX, spmv_device.cuh kSerialMax)
+(SERIAL_MAX, hspmv_internal.h kSerialMax; fp32 data: 48, kSerialMaxF32)
 they are checked BITWISE: fp32 against the reference binary's own golden
 output, fp64 against the restatement.
 """
