@@ -100,11 +100,13 @@ constexpr int32_t kLongRow = 4096;
 // one lane in the row kernels; longer ones cooperatively (fixed DPP trees) --
 // unless DevPlan.serial_max raises the bound (deterministic = 3).
 constexpr int32_t kSerialMax = 40;
-// fp32 data: 48 -- rows of 41-48 nonzeros summed serially ran 15-27 % faster
-// than in the cooperative trees (d41 113.7 -> 83.0 us, d48 106.3 -> 90.2),
-// with every other shape flat (profiles/r06s3/ab_serial48_f32.jsonl); fp64
-// rows of 48 serially met in LDS banks (d48 +41 %, r06s2), so fp64 keeps 40.
-constexpr int32_t kSerialMaxF32 = 48;
+// fp32 data: 56 -- rows of 41-56 nonzeros summed serially ran 15-27 % faster
+// than in the cooperative trees (d41 113.7 -> 83.0 us, d48 106.3 -> 90.2 at
+// 48, profiles/r06s3/ab_serial48_f32.jsonl; d50 104.7 -> 81.8, d52 100.4 ->
+// 80.4, d56 94.8 -> 80.2 at 56, r06s5), every other shape flat; 64 lost on
+// d64 (+31 %, r06s2).  fp64 rows of 48 serially met in LDS banks (d48 +41 %,
+// r06s2), so fp64 keeps 40.
+constexpr int32_t kSerialMaxF32 = 56;
 constexpr int32_t kLongChunk = 4096;
 
 // Column-sorted row blocks (csort.hip): workgroup b works on column part

@@ -327,7 +327,7 @@ typedef struct {
   int32_t deterministic;  /* HSPMV_DETERMINISTIC_*: 0 the fastest kernel
                              (CSORT's fp64 slot sums add in LDS-atomic
                              order); 1 ORDERED: only the row kernels (bit-
-                             identical run to run; rows of <= 40 (fp32: 48) nonzeros
+                             identical run to run; rows of <= 40 (fp32: 56) nonzeros
                              added in omp_spmv's order, longer ones in fixed
                              trees); 2 REPRODUCIBLE: bit-identical run to
                              run for a finite x -- CSORT then runs with
